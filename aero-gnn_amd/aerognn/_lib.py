@@ -1,0 +1,120 @@
+"""ctypes binding of libaerognn.so (C-ABI declared in include/aerognn.h).
+
+This is the drop-in boundary: every hot-path op of the reference's models/*.py is a call
+through these entry points. There is deliberately NO fallback: if the shared library is
+missing or a call fails, we raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaerognn.so")
+
+MAX_LIN = 8
+MAX_SEG = 3
+F32, BF16 = 0, 1
+SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
+
+vp = C.c_void_p
+i32 = C.c_int
+
+
+class Seg(C.Structure):
+    _fields_ = [("kind", i32), ("k", i32), ("ld", i32), ("_pad", i32),
+                ("ptr", vp), ("index", vp), ("store", vp)]
+
+
+class MlpFwdArgs(C.Structure):
+    _fields_ = [("rows", i32), ("dtype", i32), ("hidden", i32), ("nlin", i32),
+                ("out_dim", i32), ("nseg", i32), ("use_ln", i32), ("out_ld", i32),
+                ("seg", Seg * MAX_SEG),
+                ("wpk", vp * MAX_LIN), ("bias", vp * MAX_LIN),
+                ("ln_g", vp), ("ln_b", vp),
+                ("proj", vp), ("src", vp), ("dst", vp),
+                ("resid", vp), ("out", vp),
+                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp)]
+
+
+class MlpBwdArgs(C.Structure):
+    _fields_ = [("rows", i32), ("dtype", i32), ("hidden", i32), ("nlin", i32),
+                ("out_dim", i32), ("in_dim", i32), ("use_ln", i32), ("_unused", i32),
+                ("wtpk", vp * MAX_LIN), ("act", vp * MAX_LIN),
+                ("hpre", vp), ("stats", vp), ("ln_g", vp),
+                ("g", vp), ("g2", vp), ("gidx", vp),
+                ("gpre", vp * MAX_LIN),
+                ("din_nseg", i32), ("din_k", i32 * MAX_SEG),
+                ("din", vp * MAX_SEG), ("din_resid", i32 * MAX_SEG),
+                ("ln_partial", vp)]
+
+
+class PackDesc(C.Structure):
+    _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
+                ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
+                ("row_off", i32), ("col_off", i32), ("dst_rows", i32), ("dst_cols", i32)]
+
+
+_lib = None
+
+
+class AeroGNNError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libaerognn.so (raises if it has not been built: no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise AeroGNNError(
+                f"{LIB_PATH} not found: build it with `make -C aero-gnn_amd/csrc` "
+                "(or __graft_entry__.build()); the aerognn hot path has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        sig = {
+            "agn_version": (i32, []),
+            "agn_error_string": (C.c_char_p, [i32]),
+            "agn_packed_bytes": (C.c_size_t, [i32, i32, i32]),
+            "agn_pack": (i32, [vp, i32, i32, vp]),
+            "agn_mlp_forward": (i32, [C.POINTER(MlpFwdArgs), vp]),
+            "agn_mlp_bwd_nwaves": (i32, [i32]),
+            "agn_mlp_backward": (i32, [C.POINTER(MlpBwdArgs), vp]),
+            "agn_reduce_partials": (i32, [vp, i32, i32, vp, vp]),
+            "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
+            "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
+            "agn_radix_sort_temp_bytes": (C.c_size_t, [i32]),
+            "agn_radix_sort_u64": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
+            "agn_row_ptr": (i32, [vp, i32, i32, vp, vp]),
+            "agn_row_ptr_i64": (i32, [vp, i32, i32, vp, vp]),
+            "agn_exclusive_scan_i32": (i32, [vp, vp, i32, vp, vp]),
+            "agn_pool_sort_keys": (i32, [i32, vp, vp, i32, vp, vp, vp]),
+            "agn_pool_assign": (i32, [i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
+            "agn_pool_edge_candidates": (i32, [i32, vp, vp, vp, vp, vp]),
+            "agn_pool_edge_sort": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+            "agn_pool_edge_emit": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    """Names of every function include/aerognn.h declares (checked by the CPU test suite)."""
+    import re
+    hdr = os.path.join(_HERE, "..", "..", "include", "aerognn.h")
+    txt = open(hdr).read()
+    return sorted(set(re.findall(r"\b(agn_[a-z0-9_]+)\s*\(", txt)))
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().agn_error_string(rc).decode()
+        raise AeroGNNError(f"aerognn {what} failed: {msg} (code {rc})")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()

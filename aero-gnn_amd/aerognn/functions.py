@@ -1,0 +1,534 @@
+"""autograd.Functions over the libaerognn kernels: one per reference block.
+
+  MLPFn        models/mlp.py:40-51 (encoders, decoder, any MLP)
+  GMPFn        models/mgnLayer.py:177-213 (EdgeBlockSum / EdgeBlock + NodeBlock + residuals)
+  PoolNodeFn   bsms_mgn.py:265-267 scatter_mean of node latents (and pos)
+  PoolEdgeFn   bsms_mgn.py:283     scatter_mean of edge latents over coalesced edges
+  UnpoolFn     bsms_mgn.py:199-200,303-306 coarse[f2c] + skip
+
+Forward kernels write the activations the backward needs (relu outputs, pre-LN outputs and
+LN statistics); backward kernels run the chain rule per row on MFMA and the weight
+gradients are G^T X products accumulated in fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .core import (Pack, bwd_nblocks, colsum, gather_rows, mlp_backward, mlp_forward, reduce_partials,
+                   require_device, segment_sum, wgrad)
+
+
+def _c(t):
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def _ln_grads(partial, nblk, M, dtype):
+    out = torch.empty(2 * M, dtype=torch.float32, device=partial.device)
+    reduce_partials(partial, nblk, 2 * M, out)
+    return out[:M].to(dtype), out[M:].to(dtype)
+
+
+# --------------------------------------------------------------------------- chain specs
+class ChainSpec:
+    """A Linear/ReLU chain + optional LayerNorm, bound to nn.Parameters.
+
+    linears: list of (weight, bias_or_None) in order; ln: (gamma, beta) or None.
+    Pack keys: W{l} (A = W_l), T{l} (A = W_l^T), b{l}, ln_g, ln_b.
+    """
+
+    def __init__(self, linears, ln, hidden, pack: Pack, prefix=""):
+        self.linears = linears
+        self.ln = ln
+        self.hidden = hidden
+        self.nlin = len(linears)
+        self.in_dim = linears[0][0].shape[1]
+        self.out_dim = linears[-1][0].shape[0]
+        self.p = prefix
+        for l, (w, b) in enumerate(linears):
+            M, K = w.shape
+            pack.matrix(prefix + f"W{l}", M, K, [(w, 0, 0, False)])
+            pack.matrix(prefix + f"T{l}", K, M, [(w, 0, 0, True)])
+            if b is not None:
+                pack.vector(prefix + f"b{l}", M, [(b, 0)])
+        if ln is not None:
+            pack.vector(prefix + "ln_g", ln[0].numel(), [(ln[0], 0)])
+            pack.vector(prefix + "ln_b", ln[1].numel(), [(ln[1], 0)])
+        self.pack = pack
+
+    def wpk(self):
+        return [self.pack[self.p + f"W{l}"] for l in range(self.nlin)]
+
+    def wtpk(self):
+        return [self.pack[self.p + f"T{l}"] for l in range(self.nlin)]
+
+    def biases(self):
+        return [self.pack[self.p + f"b{l}"] if self.linears[l][1] is not None else None for l in range(self.nlin)]
+
+    def lnp(self):
+        return (self.pack[self.p + "ln_g"], self.pack[self.p + "ln_b"]) if self.ln is not None else None
+
+    def params(self):
+        out = []
+        for w, b in self.linears:
+            out.append(w)
+            if b is not None:
+                out.append(b)
+        if self.ln is not None:
+            out += [self.ln[0], self.ln[1]]
+        return out
+
+    def check_hidden(self):
+        H = self.hidden
+        for l, (w, b) in enumerate(self.linears):
+            M, K = w.shape
+            if l < self.nlin - 1 and M != H:
+                raise NotImplementedError(f"aerognn MLP kernels need every hidden width == {H}, got {M}")
+            if l > 0 and K != H:
+                raise NotImplementedError(f"aerognn MLP kernels need every hidden width == {H}, got {K}")
+
+
+def _alloc_saves(spec, rows, dtype, dev, train):
+    if not train:
+        return None, None, None
+    acts = [torch.empty(rows, spec.hidden, dtype=dtype, device=dev) for _ in range(spec.nlin - 1)]
+    hpre = stats = None
+    if spec.ln is not None:
+        hpre = torch.empty(rows, spec.out_dim, dtype=dtype, device=dev)
+        stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
+    return acts, hpre, stats
+
+
+def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk):
+    """Grads (in spec.params() order) from stored pre-activation grads."""
+    grads = []
+    for l, (w, b) in enumerate(spec.linears):
+        G = gpre[l]
+        if l == 0:
+            if isinstance(inputs0, (list, tuple)):
+                dw = torch.cat([wgrad(G, X) for X in inputs0], 1)
+            else:
+                dw = wgrad(G, inputs0)
+        else:
+            dw = wgrad(G, acts[l - 1])
+        grads.append(dw.to(w.dtype))
+        if b is not None:
+            grads.append(colsum(G).to(b.dtype))
+    if spec.ln is not None:
+        g, bb = _ln_grads(lnp_partial, nblk, spec.out_dim, spec.ln[0].dtype)
+        grads += [g, bb]
+    return grads
+
+
+# --------------------------------------------------------------------------- MLP
+def _ksegs(x, H):
+    """Split an input row of K features into segments of <= H (multiples of 32 but the last)."""
+    K = x.shape[1]
+    segs, k0 = [], 0
+    while k0 < K:
+        k = min(H, K - k0)
+        segs.append((k0, k))
+        k0 += k
+    return segs
+
+
+class MLPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, spec: ChainSpec, train, *params):
+        require_device(x)
+        x = _c(x)
+        rows = x.shape[0]
+        dt = x.dtype
+        out = torch.empty(rows, spec.out_dim, dtype=dt, device=x.device)
+        acts, hpre, stats = _alloc_saves(spec, rows, dt, x.device, train)
+        ks = _ksegs(x, spec.hidden)
+        if len(ks) > L.MAX_SEG:
+            raise NotImplementedError("aerognn MLP input wider than 3 x hidden")
+        segs = [(L.SEG_PLAIN, k, x.stride(0), x[:, k0:], None, None) for k0, k in ks]
+        mlp_forward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+                    segs=segs, wpk=spec.wpk(), bias=spec.biases(), ln=spec.lnp(), out=out,
+                    acts=acts, hpre=hpre, stats=stats)
+        ctx.spec = spec
+        ctx.acts, ctx.hpre, ctx.stats = acts, hpre, stats
+        ctx.save_for_backward(x)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        spec = ctx.spec
+        gy = _c(gy)
+        rows = x.shape[0]
+        dt = x.dtype
+        gpre = [torch.empty(rows, spec.hidden if l < spec.nlin - 1 else spec.out_dim, dtype=dt, device=x.device)
+                for l in range(spec.nlin)]
+        ks = _ksegs(x, spec.hidden)
+        dparts = [torch.empty(rows, k, dtype=dt, device=x.device) if ctx.needs_input_grad[0] else None
+                  for _, k in ks]
+        nblk = bwd_nblocks(rows)
+        part = torch.empty(nblk, 2 * spec.out_dim, dtype=torch.float32, device=x.device) if spec.ln else None
+        mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+                     in_dim=spec.in_dim, wtpk=spec.wtpk(), acts=ctx.acts or [], g=gy, gpre=gpre,
+                     ln_g=spec.lnp()[0] if spec.ln else None, hpre=ctx.hpre, stats=ctx.stats,
+                     din=[(k, d, False) for (_, k), d in zip(ks, dparts)], ln_partial=part)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = dparts[0] if len(dparts) == 1 else torch.cat(dparts, 1)
+        grads = _chain_param_grads(spec, gpre, x, ctx.acts, part, nblk)
+        return (dx, None, None, *grads)
+
+
+# --------------------------------------------------------------------------- GMP layer
+class LayerSpec:
+    """Binds reference blocks (mgnLayer.py:10-213) to packed operands.
+
+    Either block may be None (standalone EdgeBlock / EdgeBlockSum / NodeBlock forwards).
+    """
+
+    def __init__(self, edge_block=None, node_block=None):
+        self.pack = Pack()
+        self.edge = self.node = None
+        self.trick = False
+        self.aggregation = "add"
+        H = None
+        if node_block is not None:
+            nbm = node_block.mlp
+            self.aggregation = node_block.aggregation
+            if self.aggregation not in ("add", "mean"):
+                raise ValueError(f"Unsupported aggregation method: {self.aggregation}")  # mgnLayer.py:147-148
+            H = nbm.layers[0].weight.shape[0]
+            self.node = ChainSpec([(m.weight, m.bias) for m in nbm.layers],
+                                  (nbm.layer_norm.weight, nbm.layer_norm.bias) if nbm.use_layer_norm else None,
+                                  H, self.pack, "n")
+        if edge_block is not None:
+            eb = edge_block
+            self.trick = hasattr(eb, "edge_lin")
+            if self.trick:
+                seq = list(eb.mlp)
+                lins = [m for m in seq if isinstance(m, torch.nn.Linear)]
+                lns = [m for m in seq if isinstance(m, torch.nn.LayerNorm)]
+                He = eb.edge_lin.shape[0]
+                H = He if H is None else H
+                self.edge = ChainSpec([(eb.edge_lin, None)] + [(m.weight, m.bias) for m in lins],
+                                      (lns[0].weight, lns[0].bias) if lns else None, H, self.pack, "e")
+                node_dim = eb.src_lin.shape[1]
+                self.pack.matrix("proj", 2 * H, node_dim, [(eb.src_lin, 0, 0, False), (eb.dst_lin, H, 0, False)])
+                self.pack.matrix("projT", node_dim, 2 * H, [(eb.src_lin, 0, 0, True), (eb.dst_lin, 0, H, True)])
+                self.pack.vector("proj_b", 2 * H, [(eb.bias, H)])
+                self.eb = eb
+                if He != H or eb.src_lin.shape[0] != H:
+                    raise NotImplementedError("aerognn: edge and node hidden widths must match")
+            else:
+                em = eb.mlp
+                H = em.layers[0].weight.shape[0] if H is None else H
+                self.edge = ChainSpec([(m.weight, m.bias) for m in em.layers],
+                                      (em.layer_norm.weight, em.layer_norm.bias) if em.use_layer_norm else None,
+                                      H, self.pack, "e")
+            if getattr(eb.mlp, "activation_fn", "relu") != "relu":
+                raise NotImplementedError("aerognn kernels implement ReLU MLPs (config.yaml activation_fn)")
+        self.H = H
+        if H not in (32, 64, 128):
+            raise NotImplementedError(f"aerognn kernels support hidden 32/64/128, got {H}")
+        for c in (self.edge, self.node):
+            if c is not None:
+                c.check_hidden()
+                if c.out_dim != H:
+                    raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
+        if self.node is not None and self.node.in_dim != 2 * H:
+            raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
+        if node_block is not None and node_block.mlp.activation_fn != "relu":
+            raise NotImplementedError("aerognn kernels implement ReLU MLPs (config.yaml activation_fn)")
+
+    def edge_params(self):
+        if self.edge is None:
+            return []
+        if self.trick:
+            eb = self.eb
+            return [eb.edge_lin, eb.src_lin, eb.dst_lin, eb.bias] + self.edge.params()[1:]
+        return self.edge.params()
+
+    def node_params(self):
+        return self.node.params() if self.node is not None else []
+
+    def params(self):
+        return self.edge_params() + self.node_params()
+
+
+class GMPFn(torch.autograd.Function):
+    """x' = x + Node(x, sum_col e'), e' = e + Edge(e, x) on a CSC-ordered level."""
+
+    @staticmethod
+    def forward(ctx, x, e, level, spec: LayerSpec, train, *params):
+        require_device(x, e)
+        x, e = _c(x), _c(e)
+        dt, dev = x.dtype, x.device
+        N, E, H = x.shape[0], e.shape[0], spec.H
+        es, ns = spec.edge, spec.node
+        e_out = torch.empty_like(e)
+        x_out = torch.empty_like(x)
+        ea, ehp, est = _alloc_saves(es, E, dt, dev, train)
+        na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
+        P = None
+        if spec.trick:
+            P = torch.empty(N, 2 * H, dtype=dt, device=dev)
+            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
+                        segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
+                        wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P)
+            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+                        segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
+                        wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
+                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est)
+        else:
+            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+                        segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None),
+                              (L.SEG_GATHER, H, x.stride(0), x, level.src, None),
+                              (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)],
+                        wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), resid=e, out=e_out,
+                        acts=ea, hpre=ehp, stats=est)
+        agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
+        kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
+        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
+                    segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None),
+                          (kind, H, e_out.stride(0), e_out, level.rowptr, agg)],
+                    wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), resid=x, out=x_out,
+                    acts=na, hpre=nhp, stats=nst)
+        ctx.spec, ctx.level = spec, level
+        ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
+        ctx.save_for_backward(x, e)
+        return x_out, e_out
+
+    @staticmethod
+    def backward(ctx, gx, ge):
+        x, e = ctx.saved_tensors
+        spec, lv = ctx.spec, ctx.level
+        ea, ehp, est, na, nhp, nst, agg = ctx.saves
+        es, ns = spec.edge, spec.node
+        dt, dev = x.dtype, x.device
+        N, E, H = x.shape[0], e.shape[0], spec.H
+        gx, ge = _c(gx), _c(ge)
+        # ---- NodeBlock: d(x), d(agg)
+        gpre_n = [torch.empty(N, H, dtype=dt, device=dev) for _ in range(ns.nlin)]
+        dx = torch.empty_like(x)
+        dagg = torch.empty(N, H, dtype=dt, device=dev)
+        nb_n = bwd_nblocks(N)
+        part_n = torch.empty(nb_n, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
+        mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+                     acts=na, g=gx, gpre=gpre_n, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
+                     din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n)
+        if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
+            dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
+        # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
+        gpre_e = [torch.empty(E, H, dtype=dt, device=dev) for _ in range(es.nlin)]
+        nb_e = bwd_nblocks(E)
+        part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
+        de = torch.empty_like(e)
+        if spec.trick:
+            din = [(H, de, True)]
+        else:
+            dxs = torch.empty(E, H, dtype=dt, device=dev)
+            dxd = torch.empty(E, H, dtype=dt, device=dev)
+            din = [(H, de, True), (H, dxs, False), (H, dxd, False)]
+        mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
+                     acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
+                     hpre=ehp, stats=est, din=din, ln_partial=part_e)
+        g0 = gpre_e[0]
+        grads_edge = []
+        if spec.trick:
+            # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
+            dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
+            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
+            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
+                        segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
+                        wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
+            eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e)
+            eb = spec.eb
+            grads_edge = [eg[0], wgrad(dPs, x).to(eb.src_lin.dtype), wgrad(dPd, x).to(eb.dst_lin.dtype),
+                          colsum(dPd).to(eb.bias.dtype)] + eg[1:]
+        else:
+            ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
+            dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))
+            dx = dx + ds + dd
+            xs = x.index_select(0, lv.src.long())
+            xd = x.index_select(0, lv.dst.long())
+            grads_edge = _chain_param_grads(es, gpre_e, [e, xs, xd], ea, part_e, nb_e)
+        grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n)
+        return (dx, de, None, None, None, *grads_edge, *grads_node)
+
+
+# --------------------------------------------------------------------------- pooling
+class PoolNodeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, pool):
+        x = _c(x)
+        out = torch.empty(pool.nc, x.shape[1], dtype=x.dtype, device=x.device)
+        segment_sum(pool.nc, x.shape[1], pool.c2f_ptr, pool.c2f, x, out, mean=True)
+        ctx.pool = pool
+        ctx.n = x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p = ctx.pool
+        g = _c(g)
+        dx = torch.empty(ctx.n, g.shape[1], dtype=g.dtype, device=g.device)
+        gather_rows(ctx.n, g.shape[1], p.f2c, g, dx, cnt_ptr=p.c2f_ptr)
+        return dx, None
+
+
+class PoolEdgeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, e, pool):
+        e = _c(e)
+        ec = pool.coarse.E
+        out = torch.empty(ec, e.shape[1], dtype=e.dtype, device=e.device)
+        segment_sum(ec, e.shape[1], pool.cmem_ptr, pool.cand_sorted, e, out, mean=True)
+        ctx.pool = pool
+        ctx.n = e.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p = ctx.pool
+        g = _c(g)
+        de = torch.empty(ctx.n, g.shape[1], dtype=g.dtype, device=g.device)
+        gather_rows(ctx.n, g.shape[1], p.inv, g, de, cnt_ptr=p.cmem_ptr)
+        return de, None
+
+
+class UnpoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, coarse, skip, pool):
+        coarse, skip = _c(coarse), _c(skip)
+        n = skip.shape[0]
+        out = torch.empty_like(skip)
+        gather_rows(n, skip.shape[1], pool.f2c, coarse, out, add=skip)
+        ctx.pool = pool
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        p = ctx.pool
+        g = _c(g)
+        dc = torch.empty(p.nc, g.shape[1], dtype=g.dtype, device=g.device)
+        segment_sum(p.nc, g.shape[1], p.c2f_ptr, p.c2f, g, dc)
+        return dc, g, None
+
+
+# --------------------------------------------------------------------------- standalone blocks
+class EdgeBlockFn(torch.autograd.Function):
+    """EdgeBlockSum / EdgeBlock.forward alone (mgnLayer.py:32-49, 93-105): no residual."""
+
+    @staticmethod
+    def forward(ctx, x, e, level, spec: LayerSpec, train, *params):
+        require_device(x, e)
+        x, e = _c(x), _c(e)
+        dt, dev = x.dtype, x.device
+        N, E, H = x.shape[0], e.shape[0], spec.H
+        es = spec.edge
+        out = torch.empty(E, H, dtype=dt, device=dev)
+        ea, ehp, est = _alloc_saves(es, E, dt, dev, train)
+        if spec.trick:
+            P = torch.empty(N, 2 * H, dtype=dt, device=dev)
+            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
+                        segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
+                        wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P)
+            segs = [(L.SEG_PLAIN, H, e.stride(0), e, None, None)]
+        else:
+            P = None
+            segs = [(L.SEG_PLAIN, H, e.stride(0), e, None, None),
+                    (L.SEG_GATHER, H, x.stride(0), x, level.src, None),
+                    (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)]
+        mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, segs=segs, wpk=es.wpk(),
+                    bias=es.biases(), ln=es.lnp(), proj=P, src=level.src if P is not None else None,
+                    dst=level.dst if P is not None else None, out=out, acts=ea, hpre=ehp, stats=est)
+        ctx.spec, ctx.level, ctx.saves = spec, level, (ea, ehp, est)
+        ctx.save_for_backward(x, e)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, e = ctx.saved_tensors
+        spec, lv = ctx.spec, ctx.level
+        ea, ehp, est = ctx.saves
+        es = spec.edge
+        dt, dev = x.dtype, x.device
+        N, E, H = x.shape[0], e.shape[0], spec.H
+        g = _c(g)
+        gpre = [torch.empty(E, H, dtype=dt, device=dev) for _ in range(es.nlin)]
+        nb = bwd_nblocks(E)
+        part = torch.empty(nb, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
+        de = torch.empty_like(e)
+        if spec.trick:
+            din = [(H, de, False)]
+        else:
+            dxs = torch.empty(E, H, dtype=dt, device=dev)
+            dxd = torch.empty(E, H, dtype=dt, device=dev)
+            din = [(H, de, False), (H, dxs, False), (H, dxd, False)]
+        mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
+                     acts=ea, g=g, gpre=gpre, ln_g=es.lnp()[0] if es.ln else None, hpre=ehp, stats=est,
+                     din=din, ln_partial=part)
+        if spec.trick:
+            g0 = gpre[0]
+            dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
+            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
+            dx = torch.zeros_like(x)
+            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
+                        segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
+                        wpk=[spec.pack["projT"]], bias=[None], out=dx)
+            eg = _chain_param_grads(es, gpre, e, ea, part, nb)
+            eb = spec.eb
+            grads = [eg[0], wgrad(dPs, x).to(eb.src_lin.dtype), wgrad(dPd, x).to(eb.dst_lin.dtype),
+                     colsum(dPd).to(eb.bias.dtype)] + eg[1:]
+        else:
+            ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
+            dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))
+            dx = ds + dd
+            xs = x.index_select(0, lv.src.long())
+            xd = x.index_select(0, lv.dst.long())
+            grads = _chain_param_grads(es, gpre, [e, xs, xd], ea, part, nb)
+        return (dx, de, None, None, None, *grads)
+
+
+class NodeBlockFn(torch.autograd.Function):
+    """NodeBlock.forward alone (mgnLayer.py:134-153): mlp(cat[x, scatter(e, col)]), no residual."""
+
+    @staticmethod
+    def forward(ctx, x, e, level, spec: LayerSpec, train, *params):
+        require_device(x, e)
+        x, e = _c(x), _c(e)
+        dt, dev = x.dtype, x.device
+        N, H = x.shape[0], spec.H
+        ns = spec.node
+        out = torch.empty(N, H, dtype=dt, device=dev)
+        na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
+        agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
+        kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
+        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
+                    segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None),
+                          (kind, H, e.stride(0), e, level.rowptr, agg)],
+                    wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), out=out, acts=na, hpre=nhp, stats=nst)
+        ctx.spec, ctx.level, ctx.saves = spec, level, (na, nhp, nst, agg)
+        ctx.save_for_backward(x, e)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        x, e = ctx.saved_tensors
+        spec, lv = ctx.spec, ctx.level
+        na, nhp, nst, agg = ctx.saves
+        ns = spec.node
+        dt, dev = x.dtype, x.device
+        N, E, H = x.shape[0], e.shape[0], spec.H
+        g = _c(g)
+        gpre = [torch.empty(N, H, dtype=dt, device=dev) for _ in range(ns.nlin)]
+        dx = torch.empty_like(x)
+        dagg = torch.empty(N, H, dtype=dt, device=dev)
+        nb = bwd_nblocks(N)
+        part = torch.empty(nb, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
+        mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+                     acts=na, g=g, gpre=gpre, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
+                     din=[(H, dx, False), (H, dagg, False)], ln_partial=part)
+        de = torch.empty_like(e)
+        gather_rows(E, H, lv.dst, dagg, de, cnt_ptr=lv.rowptr if spec.aggregation == "mean" else None)
+        grads = _chain_param_grads(ns, gpre, [x, agg], na, part, nb)
+        return (dx, de, None, None, None, *grads)

@@ -1,0 +1,199 @@
+// Common device helpers for the aero-gnn MI355X (gfx950) kernels.
+//
+// Fragment convention used by every fused MLP kernel ("rows on lanes"):
+//   A wave owns 32 data rows (edges or nodes). Lane l holds data row c = l & 31 and
+//   feature half h = l >> 5. A [32 x F] activation tile lives in registers as
+//   "acc layout": register rho holds feature f(rho, h) = 8*(rho >> 2) + 4*h + (rho & 3).
+//   That is exactly the C/D layout of v_mfma_f32_32x32x{16_bf16, 2_f32} when the MFMA
+//   computes the TRANSPOSED product  Y^T[out x rows] = W[out x K] * X^T[K x rows]
+//   (col = lane & 31 = data row, row = out feature), so a layer's accumulator is fed
+//   to the next layer's MFMA as its B operand with no LDS round trip and no shuffles
+//   (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+//   The K order inside each MFMA step is permuted accordingly; weights are pre-packed
+//   into that order (pack kernel) so each lane reads its A fragment with one 16-B load.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define AGN_DEV __device__ __forceinline__
+
+namespace agn {
+
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+// ---------------------------------------------------------------- element access
+AGN_DEV float to_f(float v) { return v; }
+AGN_DEV float to_f(bf16 v) { return (float)v; }
+template <typename T> AGN_DEV T from_f(float v);
+template <> AGN_DEV float from_f<float>(float v) { return v; }
+template <> AGN_DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+
+// round-trip through storage type T (what a stored-then-reloaded value looks like)
+template <typename T> AGN_DEV float round_t(float v) { return to_f(from_f<T>(v)); }
+
+AGN_DEV f32x4 load4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+AGN_DEV f32x4 load4(const bf16* p) {
+  bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+AGN_DEV void store4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+AGN_DEV void store4(bf16* p, f32x4 v) {
+  bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  *reinterpret_cast<bf16x4*>(p) = b;
+}
+
+// Masked 4-wide load: features f0..f0+3 of a row with `k` valid features.
+template <typename T>
+AGN_DEV f32x4 load4_masked(const T* row, int f0, int k, bool vec_ok) {
+  if (vec_ok && f0 + 3 < k) return load4(row + f0);
+  f32x4 r = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (f0 + q < k) r[q] = to_f(row[f0 + q]);
+  return r;
+}
+template <typename T>
+AGN_DEV void store4_masked(T* row, int f0, int k, bool vec_ok, f32x4 v) {
+  if (vec_ok && f0 + 3 < k) { store4(row + f0, v); return; }
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (f0 + q < k) row[f0 + q] = from_f<T>(v[q]);
+}
+
+// Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
+// rows) above the MFMA chain, where they would sit live in registers across every layer.
+AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
+
+// feature index held in register rho by lane half h (acc layout)
+AGN_DEV int feat_of(int rho, int h) { return 8 * (rho >> 2) + 4 * h + (rho & 3); }
+
+// Per-feature fp32 parameter vector (bias, LN gamma/beta) in acc layout: 4-wide loads of the
+// 4 consecutive features each register quad holds. Features >= n (or p == NULL) read as 0.
+template <int NR, bool FULL = false>
+AGN_DEV void load_param(float (&v)[NR], const float* p, int n, int h) {
+#pragma unroll
+  for (int q = 0; q < NR / 4; ++q) {
+    const int f0 = 8 * q + 4 * h;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (FULL) {
+      x = *reinterpret_cast<const f32x4*>(p + f0);
+    } else if (p) {
+      if (f0 + 3 < n) x = *reinterpret_cast<const f32x4*>(p + f0);
+      else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (f0 + e < n) x[e] = p[f0 + e];
+      }
+    }
+    v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+  }
+}
+
+// ---------------------------------------------------------------- MFMA traits
+// Packed A fragments: unit u = ((ot * KU) + ku) * 64 + lane, 16 bytes per lane.
+//   bf16: one unit = one v_mfma_f32_32x32x16_bf16 k-step (16 K), KU = ceil(K/16)
+//   f32 : one unit = four v_mfma_f32_32x32x2_f32 k-steps (4 regs of B), KU = 2*ceil(K/16)
+// The number of activation registers for K features is NRK(K) = 8 * ceil(K/16).
+AGN_DEV constexpr int nrk(int k) { return 8 * ((k + 15) / 16); }
+
+// Activation operand of the next GEMM (B operand), built from acc-layout registers:
+// bf16 packs the 8 registers of one MFMA k-step (16 K) into a bf16x8; f32 keeps floats
+// (one register per v_mfma_f32_32x32x2_f32 k-step).
+template <typename T, int NR> struct BOp;
+template <int NR> struct BOp<bf16, NR> {
+  static constexpr int RPU = 8;   // registers per packed A unit
+  bf16x8 u[NR / 8];
+  AGN_DEV void set(const float (&v)[NR]) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[i][j] = (bf16)v[8 * i + j];
+  }
+  AGN_DEV void mfma(f32x16& acc, const uint4& a_raw, int unit) const {
+    bf16x8 a = *reinterpret_cast<const bf16x8*>(&a_raw);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, u[unit], acc, 0, 0, 0);
+  }
+};
+template <int NR> struct BOp<float, NR> {
+  static constexpr int RPU = 4;
+  float u[NR];
+  AGN_DEV void set(const float (&v)[NR]) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) u[i] = v[i];
+  }
+  AGN_DEV void mfma(f32x16& acc, const uint4& a_raw, int unit) const {
+    f32x4 a = *reinterpret_cast<const f32x4*>(&a_raw);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], u[4 * unit + e], acc, 0, 0, 0);
+  }
+};
+
+// Packed A fragments: unit u = ((ot * KU) + ku) * 64 + lane, 16 bytes per lane.
+//   bf16: one unit = one v_mfma_f32_32x32x16_bf16 k-step (16 K), KU = ceil(K/16)
+//   f32 : one unit = four v_mfma_f32_32x32x2_f32 k-steps, KU = 2*ceil(K/16)
+// The number of activation registers for K features is nrk(K) = 8 * ceil(K/16).
+template <typename T> AGN_DEV constexpr int units_k(int k) { return nrk(k) / BOp<T, 16>::RPU; }
+
+// acc[ot] += A[ot tile, units 0..nu-1] * B, A fragments staged in LDS as [ot][ku_total][64]
+// (16 B per lane, linear: one conflict-free ds_read_b128 per lane per unit). The next unit's
+// fragments are read while the current unit's MFMAs issue.
+template <typename T, int NT, int NR, bool FULL = false>
+AGN_DEV void gemm(f32x16 (&acc)[NT], const BOp<T, NR>& b, int nu, const uint4* lds, int ku_total,
+                  int otn, int lane) {
+  constexpr int NUMAX = NR / BOp<T, NR>::RPU;
+  uint4 ac[NT], an[NT];
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) ac[ot] = lds[(ot * ku_total) * 64 + lane];
+#pragma unroll
+  for (int u = 0; u < NUMAX; ++u) {
+    if (u < nu) {
+      if (u + 1 < nu) {
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot) an[ot] = lds[(ot * ku_total + u + 1) * 64 + lane];
+      }
+#pragma unroll
+      for (int ot = 0; ot < NT; ++ot)
+        if (FULL || ot < otn) b.mfma(acc[ot], ac[ot], u);
+#pragma unroll
+      for (int ot = 0; ot < NT; ++ot) ac[ot] = an[ot];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wave reductions
+AGN_DEV float xor32(float v) { return __shfl_xor(v, 32, 64); }
+
+// Transpose-reduce NR per-lane values over the 32 lanes of each half (lanes c = l & 31).
+// On return lane c holds in v[i] (i < max(NR/32,1)) the 32-lane sum of register
+// rho = floor(c*NR/32) + i; for NR < 32 the 32/NR lanes sharing a rho hold identical sums.
+template <int NR>
+AGN_DEV void butterfly_reduce(float (&v)[NR], int lane) {
+  const int c = lane & 31;
+  int n = NR;
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) {
+    if (n >= 2) {
+      const bool upper = (c & m) != 0;
+      const int half = n / 2;
+#pragma unroll
+      for (int i = 0; i < NR / 2; ++i) {
+        if (i < half) {
+          float keep = upper ? v[half + i] : v[i];
+          float send = upper ? v[i] : v[half + i];
+          v[i] = keep + __shfl_xor(send, m, 64);
+        }
+      }
+      n = half;
+    } else {
+      v[0] += __shfl_xor(v[0], m, 64);
+    }
+  }
+}
+
+}  // namespace agn

@@ -1,0 +1,491 @@
+// Graph-structure kernels for the MeshGraphNet hot path (gfx950): grouped (CSC/CSR) row
+// reductions, row gathers, a stable LSD radix sort, scans, and the bi-stride pooling of
+// models/bsms_mgn.py:217-306 (_downsample / _unpool_nodes).
+//
+// Determinism: no float atomics anywhere. Every reduction walks a grouped index in a fixed
+// order (for fp32 that order is the torch_scatter / scatter_add_ order of the reference), so
+// results are bitwise reproducible run to run.
+#include "common.hpp"
+#include "aerognn.h"
+
+using namespace agn;
+
+namespace {
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+// ------------------------------------------------------------------ grouped row reductions
+// out[r] = sum_{j in ptr[r]..ptr[r+1]-1} src[perm ? perm[j] : j]   (/ max(count,1) if mean)
+// 32 threads per row, 4 features per thread per pass; fp32 accumulation in index order.
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const int32_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ perm, const T* __restrict__ src,
+                                                          int src_ld, T* __restrict__ out, int out_ld, int mean) {
+  const int sub = threadIdx.x & 31;
+  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (r >= rows) return;
+  const int beg = ptr[r], end = ptr[r + 1];
+  const bool vec = ((k & 3) == 0) && ((src_ld & 3) == 0) && ((out_ld & 3) == 0);
+  for (int f0 = 4 * sub; f0 < k; f0 += 128) {
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int j = beg; j < end; ++j) {
+      const int e = perm ? perm[j] : j;
+      const f32x4 x = load4_masked(src + (size_t)e * src_ld, f0, k, vec);
+      s[0] += x[0]; s[1] += x[1]; s[2] += x[2]; s[3] += x[3];
+    }
+    if (mean) {
+      const float cnt = (float)max(end - beg, 1);
+      s[0] /= cnt; s[1] /= cnt; s[2] /= cnt; s[3] /= cnt;
+    }
+    store4_masked(out + (size_t)r * out_ld, f0, k, vec, s);
+  }
+}
+
+// out[r] = src[idx[r]] / (cnt_ptr ? max(cnt_ptr[idx+1]-cnt_ptr[idx],1) : 1) + (add ? add[r] : 0)
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const int32_t* __restrict__ idx,
+                                                          const T* __restrict__ src, int src_ld,
+                                                          const int32_t* __restrict__ cnt_ptr,
+                                                          const T* __restrict__ add, int add_ld,
+                                                          T* __restrict__ out, int out_ld) {
+  const int sub = threadIdx.x & 31;
+  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  if (r >= rows) return;
+  const int s = idx ? idx[r] : r;
+  const bool vec = ((k & 3) == 0) && ((src_ld & 3) == 0) && ((out_ld & 3) == 0) && ((add_ld & 3) == 0);
+  float div = 1.f;
+  if (cnt_ptr) div = (float)max(cnt_ptr[s + 1] - cnt_ptr[s], 1);
+  for (int f0 = 4 * sub; f0 < k; f0 += 128) {
+    f32x4 x = load4_masked(src + (size_t)s * src_ld, f0, k, vec);
+    if (cnt_ptr) { x[0] /= div; x[1] /= div; x[2] /= div; x[3] /= div; }
+    if (add) {
+      // the reference rounds the gathered value to T before the add (bsms_mgn.py:199-200)
+      const f32x4 y = load4_masked(add + (size_t)r * add_ld, f0, k, vec);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[e] = round_t<T>(x[e]) + y[e];
+    }
+    store4_masked(out + (size_t)r * out_ld, f0, k, vec, x);
+  }
+}
+
+// ------------------------------------------------------------------ stable LSD radix sort
+constexpr int RS_THREADS = 256;
+constexpr int RS_ITEMS = 8;
+constexpr int RS_TILE = RS_THREADS * RS_ITEMS;
+
+__global__ __launch_bounds__(RS_THREADS) void rs_hist_kernel(const uint64_t* __restrict__ keys, int n, int shift,
+                                                             int nblocks, int32_t* __restrict__ counts) {
+  __shared__ int32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int base = blockIdx.x * RS_TILE;
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    const int p = base + i * RS_THREADS + threadIdx.x;
+    if (p < n) atomicAdd(&h[(keys[p] >> shift) & 255], 1);
+  }
+  __syncthreads();
+  counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// exclusive scan of a single array by one block of 1024 threads (chunked per thread)
+__global__ __launch_bounds__(1024) void scan_single_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                           int n, int32_t* __restrict__ total) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (n + 1023) / 1024;
+  const int b = t * per, e = min(n, b + per);
+  int32_t s = 0;
+  for (int i = b; i < e; ++i) s += in[i];
+  part[t] = s;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    int32_t v = (t >= off) ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int32_t run = (t == 0) ? 0 : part[t - 1];
+  for (int i = b; i < e; ++i) {
+    const int32_t v = in[i];
+    out[i] = run;
+    run += v;
+  }
+  if (t == 1023 && total) *total = part[1023];
+}
+
+__global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint64_t* __restrict__ keys_in,
+                                                                const int32_t* __restrict__ vals_in, int n,
+                                                                int shift, int nblocks,
+                                                                const int32_t* __restrict__ offsets,
+                                                                uint64_t* __restrict__ keys_out,
+                                                                int32_t* __restrict__ vals_out) {
+  __shared__ int32_t base[256];
+  __shared__ int32_t wcnt[RS_THREADS / 64][256];
+  const int t = threadIdx.x;
+  const int lane = t & 63, w = t >> 6;
+  base[t] = offsets[(size_t)t * nblocks + blockIdx.x];
+  const int tile0 = blockIdx.x * RS_TILE;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    for (int wv = 0; wv < RS_THREADS / 64; ++wv) wcnt[wv][t] = 0;
+    __syncthreads();
+    const int p = tile0 + i * RS_THREADS + t;
+    const bool ok = p < n;
+    uint64_t key = 0;
+    int32_t val = 0;
+    int d = 0;
+    if (ok) {
+      key = keys_in[p];
+      val = vals_in[p];
+      d = (int)((key >> shift) & 255);
+    }
+    // peers: lanes of this wave with the same digit (8 ballots)
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t m = __ballot(ok && ((d >> bit) & 1));
+      peers &= ((d >> bit) & 1) ? m : ~m;
+    }
+    const int rank = __popcll(peers & lt);
+    if (ok && rank == 0) wcnt[w][d] = __popcll(peers);
+    __syncthreads();
+    if (ok) {
+      int pos = base[d] + rank;
+      for (int wv = 0; wv < w; ++wv) pos += wcnt[wv][d];
+      keys_out[pos] = key;
+      vals_out[pos] = val;
+    }
+    __syncthreads();
+    int tot = 0;
+#pragma unroll
+    for (int wv = 0; wv < RS_THREADS / 64; ++wv) tot += wcnt[wv][t];
+    base[t] += tot;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ misc index kernels
+__global__ void row_ptr_kernel(const int32_t* __restrict__ keys, int n, int nrows, int32_t* __restrict__ ptr) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v > nrows) return;
+  int lo = 0, hi = n;  // first i with keys[i] >= v
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  ptr[v] = lo;
+}
+
+__global__ void row_ptr64_kernel(const int64_t* __restrict__ keys, int n, int nrows, int32_t* __restrict__ ptr) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v > nrows) return;
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  ptr[v] = lo;
+}
+
+__device__ __forceinline__ uint32_t orderable(float x) {
+  const uint32_t u = __float_as_uint(x);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ void pool_keys_kernel(int n, const int64_t* __restrict__ batch, const float* __restrict__ pos, int ld,
+                                 uint64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t g = batch ? (uint64_t)batch[i] : 0ull;
+  const uint32_t lo = pos ? orderable(pos[(size_t)i * ld]) : (uint32_t)i;
+  keys[i] = (g << 32) | lo;
+  vals[i] = i;
+}
+
+// f2c[sorted[p]] = coff[g] + (p - gstart[g]) / stride,  g = batch[sorted[p]]
+__global__ void pool_f2c_kernel(int n, const int64_t* __restrict__ batch, const int32_t* __restrict__ sorted,
+                                const int32_t* __restrict__ gstart, const int32_t* __restrict__ coff, int stride,
+                                int32_t* __restrict__ f2c) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int node = sorted[p];
+  const int g = batch ? (int)batch[node] : 0;
+  f2c[node] = coff[g] + (p - gstart[g]) / stride;
+}
+
+// coarse node c: members = sorted[beg..end) re-ordered by fine node id (scatter_add order)
+__global__ void pool_members_kernel(int nc, int ngraph, const int32_t* __restrict__ sorted,
+                                    const int32_t* __restrict__ gstart, const int32_t* __restrict__ coff, int stride,
+                                    int32_t* __restrict__ c2f, int32_t* __restrict__ c2f_ptr,
+                                    int64_t* __restrict__ cbatch, int n) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nc) return;
+  if (c == nc) { c2f_ptr[nc] = n; return; }
+  int lo = 0, hi = ngraph;  // last g with coff[g] <= c
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (coff[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  const int g = lo;
+  const int beg = gstart[g] + stride * (c - coff[g]);
+  const int end = min(beg + stride, gstart[g + 1]);
+  c2f_ptr[c] = beg;
+  cbatch[c] = g;
+  for (int i = beg; i < end; ++i) c2f[i] = sorted[i];
+  for (int i = beg + 1; i < end; ++i) {  // insertion sort (stride is small)
+    const int v = c2f[i];
+    int j = i - 1;
+    while (j >= beg && c2f[j] > v) { c2f[j + 1] = c2f[j]; --j; }
+    c2f[j + 1] = v;
+  }
+}
+
+// number of fine edges whose receiver pools into coarse node c
+__global__ void pool_cand_count_kernel(int nc, const int32_t* __restrict__ c2f, const int32_t* __restrict__ c2f_ptr,
+                                       const int32_t* __restrict__ rowptr, int32_t* __restrict__ cnt) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int s = 0;
+  for (int i = c2f_ptr[c]; i < c2f_ptr[c + 1]; ++i) {
+    const int m = c2f[i];
+    s += rowptr[m + 1] - rowptr[m];
+  }
+  cnt[c] = s;
+}
+
+// flattened candidate list of coarse node c (member order, then CSC order)
+__global__ void pool_cand_list_kernel(int nc, const int32_t* __restrict__ c2f, const int32_t* __restrict__ c2f_ptr,
+                                      const int32_t* __restrict__ rowptr, const int32_t* __restrict__ cand_ptr,
+                                      int32_t* __restrict__ cand) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int o = cand_ptr[c];
+  for (int i = c2f_ptr[c]; i < c2f_ptr[c + 1]; ++i) {
+    const int m = c2f[i];
+    for (int e = rowptr[m]; e < rowptr[m + 1]; ++e) cand[o++] = e;
+  }
+}
+
+// One wave per coarse node: rank-sort its candidate fine edges by (f2c[src], refkey)
+// (refkey = the fine edge's position in the reference's own edge order at this level).
+__global__ __launch_bounds__(256) void pool_cand_sort_kernel(int nc, const int32_t* __restrict__ cand_ptr,
+                                                             const int32_t* __restrict__ cand,
+                                                             const int32_t* __restrict__ src,
+                                                             const int64_t* __restrict__ refkey,
+                                                             const int32_t* __restrict__ f2c,
+                                                             int32_t* __restrict__ sorted) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= nc) return;
+  const int b = cand_ptr[c], d = cand_ptr[c + 1] - b;
+  for (int i = lane; i < d; i += 64) {
+    const int ei = cand[b + i];
+    const int ki = f2c[src[ei]];
+    const int64_t ri = refkey[ei];
+    int rank = 0;
+    for (int j = 0; j < d; ++j) {
+      const int ej = cand[b + j];
+      const int kj = f2c[src[ej]];
+      rank += (kj < ki) || (kj == ki && refkey[ej] < ri);
+    }
+    sorted[b + rank] = ei;
+  }
+}
+
+__global__ void pool_uniq_kernel(int nc, const int32_t* __restrict__ cand_ptr, const int32_t* __restrict__ sorted,
+                                 const int32_t* __restrict__ src, const int32_t* __restrict__ f2c,
+                                 int32_t* __restrict__ uniq) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nc) return;
+  int u = 0, prev = -1;
+  for (int p = cand_ptr[c]; p < cand_ptr[c + 1]; ++p) {
+    const int k = f2c[src[sorted[p]]];
+    u += (k != prev);
+    prev = k;
+  }
+  uniq[c] = u;
+}
+
+__global__ void pool_emit_kernel(int nc, const int32_t* __restrict__ cand_ptr, const int32_t* __restrict__ sorted,
+                                 const int32_t* __restrict__ src, const int32_t* __restrict__ f2c,
+                                 const int32_t* __restrict__ crowptr, int32_t* __restrict__ csrc,
+                                 int32_t* __restrict__ cdst, int32_t* __restrict__ cmem_ptr,
+                                 int32_t* __restrict__ inv, int64_t* __restrict__ crefkey, int e_fine) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c > nc) return;
+  if (c == nc) { cmem_ptr[crowptr[nc]] = e_fine; return; }
+  int k = crowptr[c] - 1, prev = -1;
+  for (int p = cand_ptr[c]; p < cand_ptr[c + 1]; ++p) {
+    const int e = sorted[p];
+    const int s = f2c[src[e]];
+    if (s != prev) {
+      ++k;
+      csrc[k] = s;
+      cdst[k] = c;
+      cmem_ptr[k] = p;
+      crefkey[k] = (int64_t)s * nc + c;
+      prev = s;
+    }
+    inv[e] = k;
+  }
+}
+
+template <typename T>
+int seg_sum_t(int rows, int k, const int32_t* ptr, const int32_t* perm, const void* src, int src_ld, void* out,
+              int out_ld, int mean, hipStream_t st) {
+  hipLaunchKernelGGL(segment_sum_kernel<T>, dim3((rows + 7) / 8), dim3(256), 0, st, rows, k, ptr, perm,
+                     (const T*)src, src_ld, (T*)out, out_ld, mean);
+  return launch_status();
+}
+
+template <typename T>
+int gather_t(int rows, int k, const int32_t* idx, const void* src, int src_ld, const int32_t* cnt_ptr,
+             const void* add, int add_ld, void* out, int out_ld, hipStream_t st) {
+  hipLaunchKernelGGL(gather_rows_kernel<T>, dim3((rows + 7) / 8), dim3(256), 0, st, rows, k, idx, (const T*)src,
+                     src_ld, cnt_ptr, (const T*)add, add_ld, (T*)out, out_ld);
+  return launch_status();
+}
+
+inline dim3 g1(int n, int b = 256) { return dim3((n + b - 1) / b); }
+
+}  // namespace
+
+extern "C" {
+
+int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm, const void* src, int src_ld,
+                    void* out, int out_ld, int mean, void* stream) {
+  if (rows < 0 || k < 1) return AGN_E_ARG;
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == AGN_F32) return seg_sum_t<float>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
+  if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
+  return AGN_E_DTYPE;
+}
+
+int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* src, int src_ld,
+                    const int32_t* cnt_ptr, const void* add, int add_ld, void* out, int out_ld, void* stream) {
+  if (rows < 0 || k < 1) return AGN_E_ARG;
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == AGN_F32) return gather_t<float>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
+  if (dtype == AGN_BF16) return gather_t<bf16>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
+  return AGN_E_DTYPE;
+}
+
+size_t agn_radix_sort_temp_bytes(int n) {
+  const int nb = (n + RS_TILE - 1) / RS_TILE;
+  return (size_t)2 * 256 * (nb > 0 ? nb : 1) * sizeof(int32_t) + 256;
+}
+
+int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t* keys_tmp, int32_t* vals_tmp,
+                       void* scratch, void* stream) {
+  if (n < 0 || bits < 0 || bits > 64) return AGN_E_ARG;
+  if (n <= 1 || bits == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (n + RS_TILE - 1) / RS_TILE;
+  int32_t* counts = reinterpret_cast<int32_t*>(scratch);
+  int32_t* offs = counts + 256 * nb;
+  uint64_t *ki = keys, *ko = keys_tmp;
+  int32_t *vi = vals, *vo = vals_tmp;
+  const int passes = (bits + 7) / 8;
+  for (int p = 0; p < passes; ++p) {
+    const int shift = 8 * p;
+    hipLaunchKernelGGL(rs_hist_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, nb, counts);
+    hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, counts, offs, 256 * nb, (int32_t*)nullptr);
+    hipLaunchKernelGGL(rs_scatter_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, n, shift, nb, offs, ko, vo);
+    std::swap(ki, ko);
+    std::swap(vi, vo);
+  }
+  if (ki != keys) {
+    hipError_t e1 = hipMemcpyAsync(keys, ki, sizeof(uint64_t) * (size_t)n, hipMemcpyDeviceToDevice, st);
+    hipError_t e2 = hipMemcpyAsync(vals, vi, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToDevice, st);
+    if (e1 != hipSuccess) return (int)e1;
+    if (e2 != hipSuccess) return (int)e2;
+  }
+  return launch_status();
+}
+
+int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, void* stream) {
+  if (n < 0) return AGN_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    if (total) {
+      hipError_t e = hipMemsetAsync(total, 0, sizeof(int32_t), st);
+      if (e != hipSuccess) return (int)e;
+    }
+    return launch_status();
+  }
+  hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, in, out, n, total);
+  return launch_status();
+}
+
+int agn_row_ptr(const int32_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream) {
+  if (n < 0 || nrows < 0) return AGN_E_ARG;
+  hipLaunchKernelGGL(row_ptr_kernel, g1(nrows + 1), dim3(256), 0, (hipStream_t)stream, sorted_keys, n, nrows, ptr);
+  return launch_status();
+}
+
+int agn_row_ptr_i64(const int64_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream) {
+  if (n < 0 || nrows < 0) return AGN_E_ARG;
+  hipLaunchKernelGGL(row_ptr64_kernel, g1(nrows + 1), dim3(256), 0, (hipStream_t)stream, sorted_keys, n, nrows, ptr);
+  return launch_status();
+}
+
+int agn_pool_sort_keys(int n, const int64_t* batch, const float* pos, int pos_ld, uint64_t* keys, int32_t* vals,
+                       void* stream) {
+  if (n < 0) return AGN_E_ARG;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(pool_keys_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, n, batch, pos, pos_ld, keys, vals);
+  return launch_status();
+}
+
+int agn_pool_assign(int n, int nc, int ngraph, const int64_t* batch, const int32_t* sorted, const int32_t* gstart,
+                    const int32_t* coff, int stride, int32_t* f2c, int32_t* c2f, int32_t* c2f_ptr, int64_t* cbatch,
+                    void* stream) {
+  if (n < 0 || nc < 0 || stride < 1) return AGN_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0) hipLaunchKernelGGL(pool_f2c_kernel, g1(n), dim3(256), 0, st, n, batch, sorted, gstart, coff, stride, f2c);
+  hipLaunchKernelGGL(pool_members_kernel, g1(nc + 1), dim3(256), 0, st, nc, ngraph, sorted, gstart, coff, stride, c2f,
+                     c2f_ptr, cbatch, n);
+  return launch_status();
+}
+
+int agn_pool_edge_candidates(int nc, const int32_t* c2f, const int32_t* c2f_ptr, const int32_t* rowptr,
+                             int32_t* cand_cnt, void* stream) {
+  if (nc < 0) return AGN_E_ARG;
+  if (nc == 0) return 0;
+  hipLaunchKernelGGL(pool_cand_count_kernel, g1(nc), dim3(256), 0, (hipStream_t)stream, nc, c2f, c2f_ptr, rowptr,
+                     cand_cnt);
+  return launch_status();
+}
+
+int agn_pool_edge_sort(int nc, const int32_t* c2f, const int32_t* c2f_ptr, const int32_t* rowptr, const int32_t* src,
+                       const int64_t* refkey, const int32_t* f2c, const int32_t* cand_ptr, int32_t* cand_tmp,
+                       int32_t* cand_sorted, int32_t* uniq, void* stream) {
+  if (nc < 0) return AGN_E_ARG;
+  if (nc == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(pool_cand_list_kernel, g1(nc), dim3(256), 0, st, nc, c2f, c2f_ptr, rowptr, cand_ptr, cand_tmp);
+  hipLaunchKernelGGL(pool_cand_sort_kernel, dim3((nc + 3) / 4), dim3(256), 0, st, nc, cand_ptr, cand_tmp, src, refkey,
+                     f2c, cand_sorted);
+  hipLaunchKernelGGL(pool_uniq_kernel, g1(nc), dim3(256), 0, st, nc, cand_ptr, cand_sorted, src, f2c, uniq);
+  return launch_status();
+}
+
+int agn_pool_edge_emit(int nc, const int32_t* cand_ptr, const int32_t* cand_sorted, const int32_t* src,
+                       const int32_t* f2c, const int32_t* crowptr, int32_t* csrc, int32_t* cdst, int32_t* cmem_ptr,
+                       int32_t* inv, int64_t* crefkey, int e_fine, void* stream) {
+  if (nc < 0) return AGN_E_ARG;
+  hipLaunchKernelGGL(pool_emit_kernel, g1(nc + 1), dim3(256), 0, (hipStream_t)stream, nc, cand_ptr, cand_sorted, src,
+                     f2c, crowptr, csrc, cdst, cmem_ptr, inv, crefkey, e_fine);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,523 @@
+// Fused MLP chains on MFMA for the MeshGraphNet hot path (gfx950).
+//
+// One kernel evaluates a whole reference MLP — models/mlp.py:40-51 (Linear -> ReLU -> ... ->
+// Linear -> LayerNorm) — for 32 rows per wave, with the layer-0 input assembled on the fly:
+//   * EdgeBlockSum (models/mgnLayer.py:93-105): acc0 = P_s[src] + P_d[dst], input e, K = H,
+//     then ReLU/Linear chain, LN, and the residual e' = e + LN(..) of mgnLayer.py:205;
+//   * EdgeBlock    (mgnLayer.py:32-49): input cat[e, x[row], x[col]] via GATHER segments;
+//   * NodeBlock    (mgnLayer.py:134-153): input cat[x, scatter_add(e', col)] where the SUM
+//     segment reduces the receiver-grouped (CSC) rows of e' in edge order (bitwise the
+//     torch_scatter summation order for fp32), residual x' = x + .. (mgnLayer.py:211);
+//   * encoders / decoder / node projections: plain inputs.
+// Activations never leave registers between layers (see common.hpp for the layout); only
+// the block output (and, when training, the per-layer activations) are written to HBM.
+// Each layer's packed weights are staged in LDS once per 128-row block.
+#include "common.hpp"
+#include "aerognn.h"
+
+using namespace agn;
+
+namespace {
+
+constexpr int WPB = 4;           // waves per block
+constexpr int BLOCK = 64 * WPB;  // 128 data rows per block
+
+template <typename T, int NT>
+constexpr int lds_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
+
+// Stage the packed A fragments of out tiles [ot0, ot0+otn) x K units [unit0, unit0+nu) of a
+// packed matrix with `ku_total` units per tile into LDS as [otn][nu][64] (16 B each).
+AGN_DEV void stage_block(uint4* lds, const void* gw, int ku_total, int ot0, int otn, int unit0, int nu) {
+  const uint4* g = reinterpret_cast<const uint4*>(gw);
+  const int per = nu * 64;
+  const int n = otn * per;
+  for (int i = threadIdx.x; i < n; i += BLOCK) {
+    const int ot = i / per, rem = i - ot * per;
+    lds[i] = g[((size_t)(ot0 + ot) * ku_total + unit0) * 64 + rem];
+  }
+}
+
+// Row I/O in acc layout. VEC: k == 32*NT features, 16/8-byte aligned rows (no masking).
+template <typename T, int NR, bool VEC>
+AGN_DEV void load_row(float (&v)[NR], const T* rowp, int k, int h) {
+#pragma unroll
+  for (int q = 0; q < NR / 4; ++q) {
+    f32x4 x;
+    if (VEC) x = load4(rowp + 8 * q + 4 * h);
+    else x = load4_masked(rowp, 8 * q + 4 * h, k, false);
+    v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+  }
+}
+template <typename T, int NR, bool VEC>
+AGN_DEV void add_row(float (&v)[NR], const T* rowp, int k, int h) {
+#pragma unroll
+  for (int q = 0; q < NR / 4; ++q) {
+    f32x4 x;
+    if (VEC) x = load4(rowp + 8 * q + 4 * h);
+    else x = load4_masked(rowp, 8 * q + 4 * h, k, false);
+    v[4 * q] += x[0]; v[4 * q + 1] += x[1]; v[4 * q + 2] += x[2]; v[4 * q + 3] += x[3];
+  }
+}
+template <typename T, int NR, bool VEC>
+AGN_DEV void store_row(T* rowp, int k, const float (&v)[NR], int h) {
+#pragma unroll
+  for (int q = 0; q < NR / 4; ++q) {
+    const f32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    if (VEC) store4(rowp + 8 * q + 4 * h, x);
+    else store4_masked(rowp, 8 * q + 4 * h, k, false, x);
+  }
+}
+
+template <int NT, int NR>
+AGN_DEV void acc_to_regs(float (&v)[NR], const f32x16 (&acc)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[16 * t + r] = acc[t][r];
+}
+
+template <int NT, bool FULL>
+AGN_DEV void acc_bias(f32x16 (&acc)[NT], const float* b, int nvalid, int h) {
+  float v[16 * NT];
+  if (FULL && b) load_param<16 * NT, true>(v, b, nvalid, h);
+  else load_param<16 * NT, false>(v, b, nvalid, h);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = v[16 * t + r];
+}
+
+// Load one input segment for data row `rr` into acc-layout registers.
+template <typename T, int NR, bool VEC>
+AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid, int h) {
+  const T* base = reinterpret_cast<const T*>(s.ptr);
+  if (s.kind == AGN_SEG_PLAIN || s.kind == AGN_SEG_GATHER) {
+    const int r = (s.kind == AGN_SEG_GATHER) ? s.index[rr] : rr;
+    load_row<T, NR, VEC>(in, base + (size_t)r * s.ld, s.k, h);
+  } else {  // SUM / MEAN over rows index[rr] .. index[rr+1]-1 (receiver-grouped edges)
+#pragma unroll
+    for (int i = 0; i < NR; ++i) in[i] = 0.f;
+    const int beg = s.index[rr], end = s.index[rr + 1];
+    for (int j = beg; j < end; ++j) add_row<T, NR, VEC>(in, base + (size_t)j * s.ld, s.k, h);
+    if (s.kind == AGN_SEG_MEAN) {
+      const float cnt = (float)max(end - beg, 1);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) in[i] = in[i] / cnt;
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) in[i] = round_t<T>(in[i]);
+    if (s.store && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(s.store) + (size_t)rr * s.k, s.k, in, h);
+  }
+}
+
+// ------------------------------------------------------------------------- forward
+template <typename T, int NT, bool VEC>
+__global__ __launch_bounds__(BLOCK) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
+  constexpr int H = 32 * NT;
+  constexpr int NR = 16 * NT;
+  constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;  // K units of an H-wide input
+  __shared__ uint4 wl[lds_units<T, NT>()];
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int wave = blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int row = wave * 32 + c;
+  const bool valid = row < a.rows;
+  const int rr = valid ? row : a.rows - 1;
+
+  f32x16 acc[NT];
+  float v[NR];
+  BOp<T, NR> b;
+
+  int k0 = 0;
+  for (int s = 0; s < a.nseg; ++s) k0 += a.seg[s].k;
+  const int ku0 = units_k<T>(k0);
+  const int ngrp = (a.nlin == 1) ? (a.out_dim + H - 1) / H : 1;
+
+  for (int grp = 0; grp < ngrp; ++grp) {
+    const int out0 = (a.nlin == 1) ? a.out_dim : H;
+    const int gofs = grp * H;
+    const int nv0 = min(H, out0 - gofs);
+    const int otn0 = (nv0 + 31) / 32;
+    // ---- layer-0 accumulator init: bias, or the EdgeBlockSum projections gathered by src/dst
+    if (a.proj) {
+      const T* P = reinterpret_cast<const T*>(a.proj);
+      const T* ps = P + (size_t)a.src[rr] * (2 * H);
+      const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int f0 = 32 * t + 8 * q + 4 * h;
+          const f32x4 x = load4(ps + f0), y = load4(pd + f0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = x[e] + y[e];
+        }
+    } else {
+      acc_bias<NT, VEC>(acc, a.bias[0] ? a.bias[0] + gofs : nullptr, nv0, h);
+    }
+    // ---- layer 0: sum over input segments
+    int unit = 0;
+    for (int s = 0; s < a.nseg; ++s) {
+      const int nu = units_k<T>(a.seg[s].k);
+      __syncthreads();
+      stage_block(wl, a.wpk[0], ku0, grp * NT, otn0, unit, nu);
+      load_segment<T, NR, VEC>(v, a.seg[s], rr, valid, h);
+      b.set(v);
+      __syncthreads();
+      if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
+      else gemm<T, NT, NR>(acc, b, nu, wl, nu, otn0, lane);
+      unit += nu;
+    }
+    // ---- hidden layers
+    for (int l = 1; l < a.nlin; ++l) {
+      const int outl = (l == a.nlin - 1) ? a.out_dim : H;
+      const int otn = (outl + 31) / 32;
+      __syncthreads();
+      stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
+      acc_to_regs<NT, NR>(v, acc);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = fmaxf(v[i], 0.f);
+      if (a.act[l - 1] && valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, H, v, h);
+      b.set(v);
+      cbarrier();
+      acc_bias<NT, VEC>(acc, a.bias[l], outl, h);
+      __syncthreads();
+      if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
+      else gemm<T, NT, NR>(acc, b, NUH, wl, NUH, otn, lane);
+    }
+    // ---- epilogue: LayerNorm, residual, store
+    cbarrier();
+    const int outd = (a.nlin == 1) ? nv0 : a.out_dim;
+    acc_to_regs<NT, NR>(v, acc);
+    if (a.use_ln) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) s += (VEC || feat_of(i, h) < outd) ? v[i] : 0.f;
+      s += xor32(s);
+      const float mean = s / (float)outd;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const float d = v[i] - mean;
+        q += (VEC || feat_of(i, h) < outd) ? d * d : 0.f;
+      }
+      q += xor32(q);
+      const float rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
+      if (a.hpre && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.hpre) + (size_t)row * outd, outd, v, h);
+      if (a.stats && valid && h == 0) {
+        a.stats[2 * (size_t)row] = mean;
+        a.stats[2 * (size_t)row + 1] = rstd;
+      }
+float lg[NR], lb[NR];
+      load_param<NR, VEC>(lg, a.ln_g, outd, h);
+      load_param<NR, VEC>(lb, a.ln_b, outd, h);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = (v[i] - mean) * rstd * lg[i] + lb[i];
+    }
+    if (a.resid) {
+      cbarrier();
+      float r[NR];
+      load_row<T, NR, VEC>(r, reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs, outd, h);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = round_t<T>(v[i]) + r[i];
+    }
+    if (valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs, outd, v, h);
+  }
+}
+
+// ------------------------------------------------------------------------- backward
+template <typename T, int NR, bool VEC>
+AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
+  load_row<T, NR, VEC>(g, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, a.out_dim, h);
+  if (a.g2)
+    add_row<T, NR, VEC>(g, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim,
+                        a.out_dim, h);
+  if (!valid) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) g[i] = 0.f;
+  }
+}
+
+template <typename T, int NT, bool VEC>
+__global__ __launch_bounds__(BLOCK) void mlp_bwd_kernel(const agn_mlp_bwd_args a) {
+  constexpr int H = 32 * NT;
+  constexpr int NR = 16 * NT;
+  constexpr int NP = (NR >= 32) ? NR / 32 : 1;
+  __shared__ uint4 wl[lds_units<T, NT>()];
+  __shared__ float lnp[WPB][2][H];
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const int wave = blockIdx.x * WPB + wid;
+  const int row = wave * 32 + c;
+  const bool valid = row < a.rows;
+  const int rr = valid ? row : a.rows - 1;
+  const int M = a.out_dim;
+
+  float A[NR];  // current dL/d(pre-activation)
+  load_grad<T, NR, VEC>(A, a, rr, valid, h);
+  if (a.use_ln) {
+    const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
+    const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * M;
+    float B[NR];
+    load_row<T, NR, VEC>(B, hp, M, h);
+    float c1 = 0.f, c2 = 0.f;
+    float lg[NR];
+    load_param<NR, VEC>(lg, a.ln_g, M, h);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int f = feat_of(i, h);
+      const bool in = VEC || f < M;
+      B[i] = in ? (B[i] - mean) * rstd : 0.f;
+      const float gg = A[i] * lg[i];
+      c1 += gg;
+      c2 += gg * B[i];
+    }
+    c1 += xor32(c1);
+    c2 += xor32(c2);
+    c1 /= (float)M;
+    c2 /= (float)M;
+    if (a.ln_partial) {  // LayerNorm parameter partials over the wave's 32 rows (butterfly)
+#pragma unroll
+      for (int i = 0; i < NR; ++i) B[i] *= A[i];
+      butterfly_reduce<NR>(B, lane);
+      float pg[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) pg[i] = B[i];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) B[i] = A[i];
+      butterfly_reduce<NR>(B, lane);
+      const bool canon = (NR >= 32) || ((c % (32 / (NR < 32 ? NR : 32))) == 0);
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int f = feat_of((c * NR) / 32 + i, h);
+        if (canon) { lnp[wid][0][f] = pg[i]; lnp[wid][1][f] = B[i]; }
+      }
+      load_row<T, NR, VEC>(B, hp, M, h);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) B[i] = (B[i] - mean) * rstd;
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      const int f = feat_of(i, h);
+      A[i] = (VEC || f < M) ? (A[i] * lg[i] - c1 - B[i] * c2) * rstd : 0.f;
+    }
+  }
+  // chain rule through the Linear / ReLU stack
+  f32x16 acc[NT];
+  BOp<T, NR> b;
+  for (int l = a.nlin - 1; l >= 0; --l) {
+    const int Ml = (l == a.nlin - 1) ? M : H;
+    const int kuM = units_k<T>(Ml);
+    if (a.gpre[l] && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml, Ml, A, h);
+    b.set(A);
+    if (l > 0) {
+      __syncthreads();
+      stage_block(wl, a.wtpk[l], kuM, 0, NT, 0, kuM);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+      __syncthreads();
+      gemm<T, NT, NR, true>(acc, b, kuM, wl, kuM, NT, lane);
+      float m[NR];
+      cbarrier();
+      load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
+      acc_to_regs<NT, NR>(A, acc);
+#pragma unroll
+      for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? A[i] : 0.f;
+    } else {
+      int koff = 0;
+      for (int s = 0; s < a.din_nseg; ++s) {
+        const int ks = a.din_k[s];
+        if (a.din[s]) {
+          const int otn = (ks + 31) / 32;
+          __syncthreads();
+          stage_block(wl, a.wtpk[0], kuM, koff / 32, otn, 0, kuM);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+          __syncthreads();
+          gemm<T, NT, NR>(acc, b, kuM, wl, kuM, otn, lane);
+          float v[NR];
+          acc_to_regs<NT, NR>(v, acc);
+          if (a.din_resid[s]) {
+            cbarrier();
+            float g[NR];
+            load_grad<T, NR, VEC>(g, a, rr, valid, h);
+#pragma unroll
+            for (int i = 0; i < NR; ++i) v[i] += g[i];
+          }
+          if (valid) {
+            T* dp = reinterpret_cast<T*>(a.din[s]) + (size_t)row * ks;
+            if (VEC && ks == H) store_row<T, NR, true>(dp, ks, v, h);
+            else store_row<T, NR, false>(dp, ks, v, h);
+          }
+        }
+        koff += ks;
+      }
+    }
+  }
+  if (a.use_ln && a.ln_partial) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * M; i += BLOCK) {
+      const int q = i / M, f = i - q * M;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPB; ++w) s += lnp[w][q][f];
+      a.ln_partial[(size_t)blockIdx.x * 2 * M + i] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------- packing
+// A operand of Y^T = A * X^T: A[r][k] = trans ? W[k][r] : W[r][k]  (W row-major, ld)
+template <typename S>
+AGN_DEV float wat(const S* w, int ld, int M, int K, int trans, int r, int k) {
+  if (r >= M || k >= K) return 0.f;
+  return trans ? to_f(w[(size_t)k * ld + r]) : to_f(w[(size_t)r * ld + k]);
+}
+
+template <typename S>
+AGN_DEV void pack_one(const agn_pack_desc& d, int tid) {
+  const S* w = reinterpret_cast<const S*>(d.src);
+  if (d.rows == 0) {  // vector -> fp32
+    if (tid < d.cols) reinterpret_cast<float*>(d.dst)[d.col_off + tid] = to_f(w[tid]);
+    return;
+  }
+  const int OT = (d.rows + 31) / 32;
+  const int lane = tid & 63;
+  const int i = lane & 31, hh = lane >> 5;
+  const int unit = tid >> 6;
+  const int ot0 = d.row_off / 32;
+  if (d.dst_dtype == AGN_BF16) {
+    const int KU = (d.cols + 15) / 16, KUT = (d.dst_cols + 15) / 16, ku0 = d.col_off / 16;
+    if (unit >= OT * KU) return;
+    const int ot = unit / KU, ku = unit % KU;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o[j] = (bf16)wat(w, d.ld, d.rows, d.cols, d.trans, 32 * ot + i, 16 * ku + 8 * (j >> 2) + 4 * hh + (j & 3));
+    reinterpret_cast<bf16x8*>(d.dst)[((size_t)(ot0 + ot) * KUT + ku0 + ku) * 64 + lane] = o;
+  } else {
+    const int KU = 2 * ((d.cols + 15) / 16), KUT = 2 * ((d.dst_cols + 15) / 16), ku0 = d.col_off / 8;
+    if (unit >= OT * KU) return;
+    const int ot = unit / KU, ku = unit % KU;
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = wat(w, d.ld, d.rows, d.cols, d.trans, 32 * ot + i, 8 * ku + 4 * hh + e);
+    reinterpret_cast<f32x4*>(d.dst)[((size_t)(ot0 + ot) * KUT + ku0 + ku) * 64 + lane] = o;
+  }
+}
+
+__global__ void pack_kernel(const agn_pack_desc* __restrict__ descs) {
+  const agn_pack_desc d = descs[blockIdx.y];
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d.src_dtype == AGN_BF16) pack_one<bf16>(d, tid);
+  else pack_one<float>(d, tid);
+}
+
+__global__ void reduce_partials_kernel(const float* __restrict__ p, int nw, int n, float* __restrict__ out) {
+  const int cidx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cidx >= n) return;
+  float s = 0.f;
+  for (int w = 0; w < nw; ++w) s += p[(size_t)w * n + cidx];
+  out[cidx] = s;
+}
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+#define AGN_LAUNCH(KERNEL, T, NT, VEC) \
+  hipLaunchKernelGGL((KERNEL<T, NT, VEC>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a)
+
+#define AGN_DISPATCH(KERNEL)                                                       \
+  do {                                                                             \
+    if (a->dtype == AGN_F32) {                                                     \
+      if (a->hidden == 128) { if (vec) AGN_LAUNCH(KERNEL, float, 4, true); else AGN_LAUNCH(KERNEL, float, 4, false); } \
+      else if (a->hidden == 64) { if (vec) AGN_LAUNCH(KERNEL, float, 2, true); else AGN_LAUNCH(KERNEL, float, 2, false); } \
+      else if (a->hidden == 32) { if (vec) AGN_LAUNCH(KERNEL, float, 1, true); else AGN_LAUNCH(KERNEL, float, 1, false); } \
+      else return AGN_E_HIDDEN;                                                    \
+    } else if (a->dtype == AGN_BF16) {                                             \
+      if (a->hidden == 128) { if (vec) AGN_LAUNCH(KERNEL, bf16, 4, true); else AGN_LAUNCH(KERNEL, bf16, 4, false); } \
+      else if (a->hidden == 64) { if (vec) AGN_LAUNCH(KERNEL, bf16, 2, true); else AGN_LAUNCH(KERNEL, bf16, 2, false); } \
+      else if (a->hidden == 32) { if (vec) AGN_LAUNCH(KERNEL, bf16, 1, true); else AGN_LAUNCH(KERNEL, bf16, 1, false); } \
+      else return AGN_E_HIDDEN;                                                    \
+    } else {                                                                       \
+      return AGN_E_DTYPE;                                                          \
+    }                                                                              \
+  } while (0)
+
+extern "C" {
+
+int agn_version(void) { return 1; }
+
+const char* agn_error_string(int code) {
+  switch (code) {
+    case 0: return "success";
+    case AGN_E_ARG: return "invalid argument";
+    case AGN_E_DTYPE: return "unsupported dtype (f32 / bf16 only)";
+    case AGN_E_HIDDEN: return "unsupported hidden size (32, 64, 128)";
+    case AGN_E_SHAPE: return "unsupported shape";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+  }
+}
+
+size_t agn_packed_bytes(int m, int k, int dtype) {
+  return (size_t)((m + 31) / 32) * ((k + 15) / 16) * 1024 * (dtype == AGN_F32 ? 2 : 1);
+}
+
+int agn_pack(const agn_pack_desc* descs_device, int n, int max_threads, void* stream) {
+  if (n <= 0) return 0;
+  if (max_threads <= 0) return AGN_E_ARG;
+  dim3 grid((max_threads + 255) / 256, n);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, (hipStream_t)stream, descs_device);
+  return launch_status();
+}
+
+int agn_mlp_bwd_nwaves(int rows) {
+  const int waves = (rows + 31) / 32;
+  return (waves + WPB - 1) / WPB;
+}
+
+int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
+  if (!a || a->rows < 0 || a->nlin < 1 || a->nlin > AGN_MAX_LIN || a->nseg < 1 || a->nseg > AGN_MAX_SEG)
+    return AGN_E_ARG;
+  if (a->rows == 0) return 0;
+  bool vec = (a->out_ld % 4 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
+  for (int s = 0; s < a->nseg; ++s) {
+    if (a->seg[s].k < 1 || a->seg[s].k > a->hidden) return AGN_E_SHAPE;
+    if (s + 1 < a->nseg && (a->seg[s].k % 32) != 0) return AGN_E_SHAPE;
+    if (a->seg[s].k != a->hidden || a->seg[s].ld % 4 != 0) vec = false;
+  }
+  if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
+  if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
+  dim3 grid(agn_mlp_bwd_nwaves(a->rows));
+  AGN_DISPATCH(mlp_fwd_kernel);
+  return launch_status();
+}
+
+int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
+  if (!a || a->rows < 0 || a->nlin < 1 || a->nlin > AGN_MAX_LIN || a->din_nseg < 0 || a->din_nseg > AGN_MAX_SEG)
+    return AGN_E_ARG;
+  if (a->rows == 0) return 0;
+  if (a->out_dim > a->hidden) return AGN_E_SHAPE;
+  for (int s = 0; s < a->din_nseg; ++s) {
+    if (a->din_k[s] > a->hidden) return AGN_E_SHAPE;
+    if (s + 1 < a->din_nseg && (a->din_k[s] % 32) != 0) return AGN_E_SHAPE;
+  }
+  const bool vec = (a->out_dim == a->hidden);
+  dim3 grid(agn_mlp_bwd_nwaves(a->rows));
+  AGN_DISPATCH(mlp_bwd_kernel);
+  return launch_status();
+}
+
+int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     partial, nw, n, out);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+"""models/bsms_mgn.py drop-in (reference: models/bsms_mgn.py:9-306).
+
+BiStridedMeshGraphNet keeps its class name (utils.train / evaluate / AeroInference dispatch on
+`model.__class__.__name__`, utils.py:178-189), constructor, forward signature and state_dict.
+Per forward: level 0 is grouped by receiver, every bi-stride pooling map (x-sort, stride
+contraction, edge coalescing) is built on the GPU by libaerognn, then the U-Net runs
+fused GMP layers, mean-pool / unpool+skip kernels, and the decoder.
+"""
+import torch
+from torch import nn
+
+from aerognn.functions import PoolEdgeFn, PoolNodeFn, UnpoolFn
+from aerognn.graph import Level, downsample_maps
+from aerognn.core import require_device, segment_sum
+from models.mlp import MLP
+from models.mgnLayer import MeshGraphNetLayer
+
+
+class BiStridedMeshGraphNet(nn.Module):
+    """Multi-scale MeshGraphNet using bi-strided pooling and skip connections."""
+
+    def __init__(self, input_node_dim: int, input_edge_dim: int, output_node_dim: int, processor_size: int = 15,
+                 activation_fn: str = "relu", num_hidden_layers_node_processor: int = 1,
+                 num_hidden_layers_edge_processor: int = 1, hidden_dim_processor: int = 128,
+                 num_hidden_layers_node_encoder: int = 1, hidden_dim_node_encoder: int = 128,
+                 num_hidden_layers_edge_encoder: int = 1, hidden_dim_edge_encoder: int = 128,
+                 aggregation: str = "add", hidden_dim_decoder: int = 128, num_hidden_layers_decoder: int = 1,
+                 dropout: float = 0.0, do_concat_trick: bool = False, num_scales: int = 3,
+                 layers_per_scale: int = 2, stride: int = 2) -> None:
+        super().__init__()
+        if num_scales < 1:
+            raise ValueError("num_scales must be >= 1")
+        if stride < 1:
+            raise ValueError("stride must be >= 1")
+        self.num_scales = num_scales
+        self.stride = stride
+        self.aggregation = aggregation
+        self.do_concat_trick = do_concat_trick
+        self.node_encoder = MLP(input_dim=input_node_dim, hidden_dim=hidden_dim_node_encoder,
+                                output_dim=hidden_dim_processor, num_hidden_layers=num_hidden_layers_node_encoder,
+                                activation_fn=activation_fn, dropout=dropout, use_layer_norm=True)
+        self.edge_encoder = MLP(input_dim=input_edge_dim, hidden_dim=hidden_dim_edge_encoder,
+                                output_dim=hidden_dim_processor, num_hidden_layers=num_hidden_layers_edge_encoder,
+                                activation_fn=activation_fn, dropout=dropout, use_layer_norm=True)
+        if isinstance(layers_per_scale, int):
+            down_counts = [layers_per_scale for _ in range(max(num_scales - 1, 0))]
+            up_counts = [layers_per_scale for _ in range(max(num_scales - 1, 0))]
+        else:
+            if len(layers_per_scale) != max(num_scales - 1, 0):
+                raise ValueError("layers_per_scale must be int or list with num_scales-1 elements")
+            down_counts = list(layers_per_scale)
+            up_counts = list(layers_per_scale)
+        used_layers = 2 * sum(down_counts)
+        bottleneck_layers = max(1, processor_size - used_layers)
+
+        def _build_block(num_layers: int) -> nn.ModuleList:
+            return nn.ModuleList([
+                MeshGraphNetLayer(node_dim=hidden_dim_processor, edge_dim=hidden_dim_processor,
+                                  hidden_dim=hidden_dim_processor,
+                                  num_hidden_layers_node_processor=num_hidden_layers_node_processor,
+                                  num_hidden_layers_edge_processor=num_hidden_layers_edge_processor,
+                                  activation_fn=activation_fn, use_layer_norm=True, aggregation=aggregation,
+                                  do_concat_trick=do_concat_trick)
+                for _ in range(num_layers)])
+
+        self.down_layers = nn.ModuleList([_build_block(count) for count in down_counts])
+        self.bottleneck_layers = _build_block(bottleneck_layers)
+        self.up_layers = nn.ModuleList([_build_block(count) for count in reversed(up_counts)])
+        self.decoder = MLP(input_dim=hidden_dim_processor, hidden_dim=hidden_dim_decoder, output_dim=output_node_dim,
+                           num_hidden_layers=num_hidden_layers_decoder, activation_fn=activation_fn,
+                           use_layer_norm=False)
+        self.dropout = nn.Dropout(dropout) if dropout > 0 else None
+
+    # ------------------------------------------------------------------ hierarchy (index maps)
+    def _hierarchy(self, edge_index, batch, pos, n):
+        """Level 0 + one Pooling per down scale (bsms_mgn.py:155-185 order)."""
+        level = Level.from_edge_index(edge_index, n)
+        ngraph = 1 if batch is None else int(batch[-1].item()) + 1 if n > 0 else 1
+        pools = []
+        cb, cp, lv = batch, pos, level
+        for _ in range(len(self.down_layers)):
+            P = downsample_maps(lv, cb, cp, self.stride, ngraph)
+            if cp is not None:  # coarse pos = scatter_mean(pos, f2c) (bsms_mgn.py:269-274), fp32
+                cp32 = cp if cp.dtype == torch.float32 else cp.float()
+                cpos = torch.empty(P.nc, cp32.shape[1], dtype=torch.float32, device=cp32.device)
+                segment_sum(P.nc, cp32.shape[1], P.c2f_ptr, P.c2f, cp32.contiguous(), cpos, mean=True)
+                P.cpos = cpos
+            else:
+                P.cpos = None
+            pools.append(P)
+            cb, cp, lv = P.cbatch, P.cpos, P.coarse
+        return level, pools
+
+    def forward(self, node_attr: torch.Tensor, edge_attr: torch.Tensor, edge_index: torch.Tensor,
+                batch: torch.Tensor = None, pos: torch.Tensor = None) -> torch.Tensor:
+        require_device(node_attr, edge_attr, edge_index, batch, pos)
+        n = node_attr.size(0)
+        level, pools = self._hierarchy(edge_index, batch, pos, n)
+        node_hidden = self.node_encoder(node_attr)
+        edge_hidden = self.edge_encoder(edge_attr[level.perm])
+        if self.dropout is not None:
+            node_hidden = self.dropout(node_hidden)
+            edge_hidden = self.dropout(edge_hidden)
+        skips = []
+        cn, ce, lv = node_hidden, edge_hidden, level
+        for scale_idx, layers in enumerate(self.down_layers):
+            for layer in layers:
+                cn, ce = layer.forward_level(cn, ce, lv)
+            skips.append((cn, ce, lv))
+            P = pools[scale_idx]
+            cn = PoolNodeFn.apply(cn, P)
+            ce = PoolEdgeFn.apply(ce, P)
+            lv = P.coarse
+        for layer in self.bottleneck_layers:
+            cn, ce = layer.forward_level(cn, ce, lv)
+        for scale_idx, layers in enumerate(self.up_layers):
+            if pools:
+                sn, se, slv = skips[-(scale_idx + 1)]
+                cn = UnpoolFn.apply(cn, sn, pools[-(scale_idx + 1)])   # coarse[f2c] + skip
+                ce, lv = se, slv                                        # fine edges restored
+            for layer in layers:
+                cn, ce = layer.forward_level(cn, ce, lv)
+        return self.decoder(cn)
+
+    def _downsample(self, node_attr, edge_attr, edge_index, batch, pos=None):
+        """Reference-format _downsample (bsms_mgn.py:217-301): coarse edges sorted by (row, col)."""
+        require_device(node_attr, edge_attr, edge_index, batch, pos)
+        n = node_attr.size(0)
+        level = Level.from_edge_index(edge_index, n)
+        ngraph = int(batch[-1].item()) + 1 if n > 0 else 1
+        P = downsample_maps(level, batch, pos, self.stride, ngraph)
+        cnode = PoolNodeFn.apply(node_attr, P)
+        cedge_csc = PoolEdgeFn.apply(edge_attr[level.perm], P)
+        cpos = None
+        if pos is not None:
+            cpos = PoolNodeFn.apply(pos.float().contiguous(), P).to(pos.dtype)
+        order = P.coarse.perm_src.long()  # CSC -> (row, col) lexicographic (torch.unique order)
+        cei = torch.stack([P.coarse.src[order].long(), P.coarse.dst[order].long()], 0)
+        return cnode, cedge_csc[order], cei, P.cbatch, cpos, P.f2c.long()
+
+    def _unpool_nodes(self, coarse_nodes: torch.Tensor, assignment: torch.Tensor) -> torch.Tensor:
+        return coarse_nodes[assignment]

@@ -1,0 +1,163 @@
+"""models/mgnLayer.py drop-in (reference: models/mgnLayer.py:1-213).
+
+Parameters, their init order and state_dict keys are the reference's. Forward passes run in
+libaerognn: EdgeBlockSum/EdgeBlock/NodeBlock alone through EdgeBlockFn/NodeBlockFn, and a
+whole MeshGraphNetLayer (edge update + receiver aggregation + node update + residuals,
+mgnLayer.py:177-213) through the fused GMPFn. Edges are processed receiver-grouped (CSC);
+results come back in the caller's edge order.
+"""
+import os
+
+import torch
+from torch import nn
+
+from aerognn.functions import EdgeBlockFn, GMPFn, LayerSpec, NodeBlockFn
+from aerognn.graph import Level
+from models.mlp import MLP
+
+
+def _level(edge_index, n):
+    return Level.from_edge_index(edge_index, n)
+
+
+class EdgeBlock(nn.Module):
+    """Edge processing block for MeshGraphNet (mgnLayer.py:10-49)."""
+
+    def __init__(self, node_dim: int, edge_dim: int, hidden_dim: int = 128, num_hidden_layers: int = 1,
+                 activation_fn: str = 'relu', use_layer_norm: bool = True):
+        super().__init__()
+        input_dim = edge_dim + 2 * node_dim
+        self.mlp = MLP(input_dim=input_dim, hidden_dim=hidden_dim, output_dim=edge_dim,
+                       num_hidden_layers=num_hidden_layers, activation_fn=activation_fn,
+                       use_layer_norm=use_layer_norm)
+        self._spec = None
+
+    def spec(self):
+        if self._spec is None:
+            self._spec = LayerSpec(edge_block=self)
+        return self._spec
+
+    def forward(self, edge_attr, node_attr, edge_index):
+        s = self.spec()
+        lv = _level(edge_index, node_attr.shape[0])
+        s.pack.update(node_attr.dtype, node_attr.device)
+        out = EdgeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.edge_params())
+        return out[lv.perm_inv]
+
+
+class EdgeBlockSum(nn.Module):
+    """Sum trick + pre-project nodes (mgnLayer.py:51-105):
+    h0 = W_e e + (W_s x)[row] + (W_d x)[col] + b, then ReLU/Linear chain + LN."""
+
+    def __init__(self, node_dim: int, edge_dim: int, hidden_dim: int = 128, num_hidden_layers: int = 1,
+                 activation_fn: str = 'relu', use_layer_norm: bool = True):
+        super().__init__()
+        self.edge_dim = edge_dim
+        self.src_dim = node_dim
+        self.dst_dim = node_dim
+        tmp_lin = nn.Linear(self.edge_dim + self.src_dim + self.dst_dim, hidden_dim, bias=True)
+        orig_weight = tmp_lin.weight.data
+        w_e, w_s, w_d = torch.split(orig_weight, [self.edge_dim, self.src_dim, self.dst_dim], dim=1)
+        # contiguous copies: the reference keeps strided views of tmp_lin.weight (mgnLayer.py:74-79);
+        # values and state_dict are identical, the packed-weight kernel needs dense rows
+        self.edge_lin = nn.Parameter(w_e.contiguous())
+        self.src_lin = nn.Parameter(w_s.contiguous())
+        self.dst_lin = nn.Parameter(w_d.contiguous())
+        self.bias = tmp_lin.bias
+        activation = nn.ReLU()  # activation_fn is ignored, as in the reference (mgnLayer.py:81)
+        layers = [activation]
+        self.num_hidden_layers = num_hidden_layers
+        for _ in range(num_hidden_layers):
+            layers += [nn.Linear(hidden_dim, hidden_dim), activation]
+        layers.append(nn.Linear(hidden_dim, edge_dim))
+        if use_layer_norm:
+            layers.append(nn.LayerNorm(edge_dim))
+        self.mlp = nn.Sequential(*layers)
+        self._spec = None
+
+    def spec(self):
+        if self._spec is None:
+            self._spec = LayerSpec(edge_block=self)
+        return self._spec
+
+    def forward(self, edge_attr, node_attr, edge_index):
+        s = self.spec()
+        lv = _level(edge_index, node_attr.shape[0])
+        s.pack.update(node_attr.dtype, node_attr.device)
+        out = EdgeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.edge_params())
+        return out[lv.perm_inv]
+
+
+class NodeBlock(nn.Module):
+    """Node processing block for MeshGraphNet (mgnLayer.py:111-153)."""
+
+    def __init__(self, node_dim: int, edge_dim: int, hidden_dim: int = 128, num_hidden_layers: int = 1,
+                 activation_fn: str = 'relu', use_layer_norm: bool = True, aggregation: str = 'add'):
+        super().__init__()
+        input_dim = node_dim + edge_dim
+        self.aggregation = aggregation
+        self.mlp = MLP(input_dim=input_dim, hidden_dim=hidden_dim, output_dim=node_dim,
+                       num_hidden_layers=num_hidden_layers, activation_fn=activation_fn,
+                       use_layer_norm=use_layer_norm)
+        self._spec = None
+
+    def spec(self):
+        if self._spec is None:
+            self._spec = LayerSpec(node_block=self)
+        return self._spec
+
+    def forward(self, node_attr, edge_attr, edge_index):
+        if self.aggregation not in ('mean', 'add'):
+            raise ValueError(f"Unsupported aggregation method: {self.aggregation}")
+        s = self.spec()
+        lv = _level(edge_index, node_attr.shape[0])
+        s.pack.update(node_attr.dtype, node_attr.device)
+        return NodeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.node_params())
+
+
+_MEMLOG = os.environ.get("AEROGNN_MEMLOG", "1") != "0"
+
+
+class MeshGraphNetLayer(nn.Module):
+    """Single layer of MeshGraphNet with edge and node processing blocks (mgnLayer.py:156-213)."""
+
+    def __init__(self, node_dim: int, edge_dim: int, hidden_dim: int = 128,
+                 num_hidden_layers_node_processor: int = 1, num_hidden_layers_edge_processor: int = 1,
+                 activation_fn: str = 'relu', use_layer_norm: bool = True, aggregation: str = 'add',
+                 do_concat_trick: bool = False):
+        super().__init__()
+        if do_concat_trick:
+            self.edge_block = EdgeBlockSum(node_dim, edge_dim, hidden_dim, num_hidden_layers_edge_processor,
+                                           activation_fn, use_layer_norm)
+        else:
+            self.edge_block = EdgeBlock(node_dim, edge_dim, hidden_dim, num_hidden_layers_edge_processor,
+                                        activation_fn, use_layer_norm)
+        self.node_block = NodeBlock(node_dim, edge_dim, hidden_dim, num_hidden_layers_node_processor,
+                                    activation_fn, use_layer_norm, aggregation)
+        self._spec = None
+
+    def spec(self):
+        if self._spec is None:
+            if self.node_block.aggregation not in ('mean', 'add'):
+                raise ValueError(f"Unsupported aggregation method: {self.node_block.aggregation}")
+            self._spec = LayerSpec(self.edge_block, self.node_block)
+        return self._spec
+
+    def forward_level(self, node_attr, edge_attr, level):
+        """Hot path: edge latents already in the level's receiver-grouped (CSC) order."""
+        s = self.spec()
+        s.pack.update(node_attr.dtype, node_attr.device)
+        if _MEMLOG and not hasattr(self, '_edge_block_mem_logged'):
+            # the reference prints its EdgeBlock memory delta once per layer (mgnLayer.py:185-203)
+            before = torch.cuda.memory_allocated() / (1024 ** 2)
+            x, e = GMPFn.apply(node_attr, edge_attr, level, s, torch.is_grad_enabled(), *s.params())
+            print(f"EdgeBlock - Allocated: {torch.cuda.memory_allocated() / (1024 ** 2) - before:.2f} MB, "
+                  f"Peak increase: {0.0:.2f} MB")
+            self._edge_block_mem_logged = True
+            return x, e
+        return GMPFn.apply(node_attr, edge_attr, level, s, torch.is_grad_enabled(), *s.params())
+
+    def forward(self, node_attr, edge_attr, edge_index):
+        lv = _level(edge_index, node_attr.shape[0])
+        x, e = self.forward_level(node_attr, edge_attr[lv.perm], lv)
+        return x, e[lv.perm_inv]

@@ -1,0 +1,56 @@
+"""models/mlp.py drop-in (reference: models/mlp.py:5-51).
+
+Module tree and parameter init order are the reference's (so torch.manual_seed gives the
+same initial weights); forward runs the whole Linear/ReLU/.../LayerNorm chain as ONE fused
+libaerognn kernel (aerognn.functions.MLPFn).
+"""
+import torch
+from torch import nn
+import torch.nn.functional as F
+
+from aerognn.core import Pack
+from aerognn.functions import ChainSpec, MLPFn
+
+
+class MLP(nn.Module):
+    """Multi-Layer Perceptron with configurable layers and activation."""
+
+    def __init__(self, input_dim: int, hidden_dim: int, output_dim: int, num_hidden_layers: int = 1,
+                 activation_fn: str = 'relu', dropout: float = 0.0, use_layer_norm: bool = True):
+        super().__init__()
+        self.layers = nn.ModuleList()
+        self.use_layer_norm = use_layer_norm
+        self.layers.append(nn.Linear(input_dim, hidden_dim))                  # mlp.py:22
+        for _ in range(num_hidden_layers):
+            self.layers.append(nn.Linear(hidden_dim, hidden_dim))             # mlp.py:25-26
+        if num_hidden_layers > 0:
+            self.layers.append(nn.Linear(hidden_dim, output_dim))             # mlp.py:29-30
+        else:
+            self.layers[-1] = nn.Linear(input_dim, output_dim)                # mlp.py:31-32 quirk
+        if use_layer_norm:
+            self.layer_norm = nn.LayerNorm(output_dim)
+        self.activation = getattr(F, activation_fn)
+        self.dropout = nn.Dropout(dropout)
+        self.hidden_dim = hidden_dim
+        self.activation_fn = activation_fn
+        self._spec = None
+
+    def spec(self):
+        if self._spec is None:
+            if self.activation_fn != 'relu':
+                raise NotImplementedError("aerognn fused MLP implements activation_fn='relu' (config.yaml)")
+            H = self.hidden_dim if len(self.layers) > 1 else max(32, ((self.layers[0].weight.shape[0] + 31) // 32) * 32)
+            if H not in (32, 64, 128):
+                raise NotImplementedError(f"aerognn fused MLP supports hidden_dim 32/64/128, got {H}")
+            lins = [(m.weight, m.bias) for m in self.layers]
+            ln = (self.layer_norm.weight, self.layer_norm.bias) if self.use_layer_norm else None
+            self._spec = ChainSpec(lins, ln, H, Pack())
+            self._spec.check_hidden()
+        return self._spec
+
+    def forward(self, x):
+        if self.training and self.dropout.p > 0:
+            raise NotImplementedError("aerognn fused MLP: dropout > 0 in training is not implemented")
+        s = self.spec()
+        s.pack.update(x.dtype, x.device)
+        return MLPFn.apply(x, s, torch.is_grad_enabled(), *s.params())

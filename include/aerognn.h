@@ -1,0 +1,192 @@
+/* aerognn.h — C-ABI of libaerognn.so, the MI355X (gfx950) hot path of the bi-stride
+ * multi-scale MeshGraphNet (cudagu/aero-gnn).
+ *
+ * The reference is pure Python + PyTorch/torch_scatter: it has no FFI of its own.
+ * Each entry point below replaces the aten / torch_scatter work that one reference Python
+ * call performs; the Python mirror (aero-gnn_amd/models/) binds them with ctypes
+ * (aero-gnn_amd/aerognn/_lib.py). Plain pointers and sizes only; every device pointer is
+ * HBM memory owned by the caller; `stream` is a hipStream_t (NULL = default stream).
+ * Return value: 0 on success, a hipError_t (>0) from the launch, or a negative AGN_E*
+ * argument error (see agn_error_string).
+ *
+ * Replaces (reference file:line) --
+ *   agn_mlp_forward   models/mlp.py:40-51 MLP.forward; models/mgnLayer.py:93-105 EdgeBlockSum
+ *                     (+ gather of mgnLayer.py:103, residual :205); mgnLayer.py:32-49 EdgeBlock;
+ *                     mgnLayer.py:134-153 NodeBlock incl. torch_scatter.scatter_add/mean (:144,146)
+ *                     and the residual of :211
+ *   agn_mlp_backward  autograd of the same
+ *   agn_segment_sum   torch_scatter scatter_add/scatter_mean over a grouped (CSR/CSC) index:
+ *                     mgnLayer.py:144-146 backward of index (:103), bsms_mgn.py:265,270,283
+ *   agn_gather_rows   bsms_mgn.py:303-306 (_unpool_nodes) + :200 skip add; backward of
+ *                     scatter_mean (gather / count)
+ *   agn_radix_sort_*  bsms_mgn.py:242 torch.argsort(pos[:,0]) per graph (stable tie rule),
+ *                     :280 torch.unique(keys) ordering; CSC/CSR construction for aggregation
+ *   agn_pool_*        bsms_mgn.py:217-301 (_downsample: index map, coarse edge coalesce, means)
+ *   agn_pack          layout conversion of nn.Linear weights into MFMA A-fragments
+ */
+#ifndef AEROGNN_H
+#define AEROGNN_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AGN_MAX_LIN 8
+#define AGN_MAX_SEG 3
+
+enum { AGN_F32 = 0, AGN_BF16 = 1 };
+enum { AGN_SEG_PLAIN = 0, AGN_SEG_GATHER = 1, AGN_SEG_SUM = 2, AGN_SEG_MEAN = 3 };
+enum { AGN_E_ARG = -1, AGN_E_DTYPE = -2, AGN_E_HIDDEN = -3, AGN_E_SHAPE = -4 };
+
+/* One input segment of a concatenated MLP input row (torch.cat in mgnLayer.py:44,151).
+ * PLAIN : row r of ptr;  GATHER: row index[r] of ptr (x[row], x[col] of mgnLayer.py:40-41);
+ * SUM/MEAN: sum (mean) of rows index[r] .. index[r+1]-1 of ptr (scatter_add / scatter_mean
+ * of dst-grouped edges: index = CSC row pointer, rows grouped by receiver). */
+typedef struct {
+  int kind;
+  int k;          /* features in this segment (<= hidden) */
+  int ld;         /* row stride of ptr, elements */
+  int _pad;
+  const void* ptr;
+  const int32_t* index;
+  void* store;    /* optional: write the segment value (e.g. aggregated edges) [rows][k] */
+} agn_seg;
+
+typedef struct {
+  int rows;
+  int dtype;       /* activation storage dtype AGN_F32 / AGN_BF16 */
+  int hidden;      /* 32, 64 or 128 */
+  int nlin;        /* Linear layers in the chain (1..AGN_MAX_LIN), ReLU between */
+  int out_dim;     /* features of the last Linear */
+  int nseg;        /* input segments of layer 0 */
+  int use_ln;      /* LayerNorm(out_dim) after the last Linear, eps 1e-5 */
+  int out_ld;
+  agn_seg seg[AGN_MAX_SEG];
+  const void* wpk[AGN_MAX_LIN];    /* packed weights (agn_pack, trans = 0) */
+  const float* bias[AGN_MAX_LIN];  /* fp32 bias or NULL */
+  const float* ln_g;
+  const float* ln_b;
+  /* EdgeBlockSum prologue: layer-0 accumulator starts at P[src][0:H] + P[dst][H:2H] */
+  const void* proj;                /* [*][2H] = [x W_s^T | x W_d^T + b] or NULL */
+  const int32_t* src;
+  const int32_t* dst;
+  const void* resid;               /* y = resid + mlp(...) (row-major, ld = out_ld) or NULL */
+  void* out;
+  /* training saves (NULL when not needed) */
+  void* act[AGN_MAX_LIN];          /* relu output of layer l (l < nlin-1), [rows][hidden] */
+  void* hpre;                      /* last Linear output before LN, [rows][out_dim] */
+  float* stats;                    /* [rows][2] = mean, rstd */
+} agn_mlp_fwd_args;
+
+typedef struct {
+  int rows;
+  int dtype;
+  int hidden;
+  int nlin;
+  int out_dim;
+  int in_dim;      /* K of layer 0 (sum of segment widths in forward) */
+  int use_ln;
+  int _unused;
+  const void* wtpk[AGN_MAX_LIN];   /* packed TRANSPOSED weights (agn_pack, trans = 1) */
+  const void* act[AGN_MAX_LIN];
+  const void* hpre;
+  const float* stats;
+  const float* ln_g;
+  /* upstream gradient of the MLP output (+ optional gathered add: g2[gidx[r]]) */
+  const void* g;
+  const void* g2;
+  const int32_t* gidx;
+  /* outputs */
+  void* gpre[AGN_MAX_LIN];         /* dL/d(pre-activation of layer l), [rows][M_l] */
+  int din_nseg;                    /* segments of d(input of layer 0): widths din_k[s] */
+  int din_k[AGN_MAX_SEG];
+  void* din[AGN_MAX_SEG];          /* NULL = not needed */
+  int din_resid[AGN_MAX_SEG];      /* 1: din[s] = g(+g2) + W0^T dh0 (residual of the block) */
+  float* ln_partial;               /* [agn_mlp_bwd_nwaves(rows)][2][out_dim]: sum g*xhat, sum g */
+} agn_mlp_bwd_args;
+
+/* Pack an A operand A[r][k] = trans ? W[k][r] : W[r][k] (r < rows, k < cols) into rows
+ * [row_off, row_off+rows) x cols [col_off, col_off+cols) of a packed [dst_rows x dst_cols]
+ * operand (row_off % 32 == 0, col_off % 16 == 0), so separate nn.Parameters (EdgeBlockSum's
+ * src_lin / dst_lin, mgnLayer.py:122-129) pack into one concatenated operand. rows == 0:
+ * copy a vector of `cols` values to fp32 at dst + col_off floats. */
+typedef struct {
+  const void* src;
+  void* dst;
+  int src_dtype;
+  int dst_dtype;
+  int rows;
+  int cols;
+  int trans;
+  int ld;            /* row stride of W (elements) */
+  int row_off;
+  int col_off;
+  int dst_rows;
+  int dst_cols;
+} agn_pack_desc;
+
+int agn_version(void);
+const char* agn_error_string(int code);
+/* bytes of a packed A operand with `m` rows and `k` reduction columns */
+size_t agn_packed_bytes(int m, int k, int dtype);
+/* max_threads >= max over descs of packed 16-B units (or vector length) */
+int agn_pack(const agn_pack_desc* descs_device, int n, int max_threads, void* stream);
+
+int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream);
+/* rows of ln_partial written by agn_mlp_backward (one per 256-row block) */
+int agn_mlp_bwd_nwaves(int rows);
+int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream);
+/* out[c] = sum_w partial[w][c], c < n, fixed order (deterministic LN parameter grads) */
+int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* stream);
+
+/* out[r] = sum (or mean) of src[perm ? perm[j] : j] for j in ptr[r]..ptr[r+1]-1; [rows][k] */
+int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm,
+                    const void* src, int src_ld, void* out, int out_ld, int mean, void* stream);
+/* out[r] = src[idx[r]] * (inv_count ? 1/max(cnt[idx[r]],1) : 1) + (add ? add[r] : 0) */
+int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* src, int src_ld,
+                    const int32_t* cnt_ptr, const void* add, int add_ld, void* out, int out_ld,
+                    void* stream);
+
+/* Stable LSD radix sort of (key, value) pairs on `bits` low key bits. tmp buffers hold n each;
+ * agn_radix_sort_temp_bytes gives the scratch size. Result ends in keys/vals. */
+size_t agn_radix_sort_temp_bytes(int n);
+int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t* keys_tmp,
+                       int32_t* vals_tmp, void* scratch, void* stream);
+/* CSR row pointer of sorted int keys: ptr[v] = first i with key[i] >= v, v = 0..nrows */
+int agn_row_ptr(const int32_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream);
+
+/* exclusive prefix sum of n int32 (single launch); *total (optional) = sum */
+int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, void* stream);
+/* same as agn_row_ptr for sorted int64 keys (PyG `batch` vectors) */
+int agn_row_ptr_i64(const int64_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream);
+
+/* ---- bi-stride pooling (bsms_mgn.py:217-301) ----
+ * 1. agn_pool_sort_keys + agn_radix_sort_u64: nodes ordered by (graph, x) — the per-graph
+ *    argsort(pos[:,0]) of bsms_mgn.py:240-243 with the stable (x, node id) tie rule; pos == NULL
+ *    keeps node order (bsms_mgn.py:244-245).
+ * 2. agn_pool_assign: f2c = rank // stride + coarse offset of the graph (bsms_mgn.py:247-256),
+ *    coarse members grouped per coarse node in ascending fine id (c2f, c2f_ptr), coarse batch.
+ * 3. agn_pool_edge_candidates / _sort / _emit: coarse edge coalescing (bsms_mgn.py:276-288):
+ *    per coarse receiver, the fine edges of its members sorted by (f2c[src], reference order)
+ *    and run-length encoded -> coarse CSC (csrc, cdst), member ranges (cmem_ptr into cand_sorted),
+ *    inverse map, and the coarse level's reference-order key (row * Nc + col). */
+int agn_pool_sort_keys(int n, const int64_t* batch, const float* pos, int pos_ld, uint64_t* keys,
+                       int32_t* vals, void* stream);
+int agn_pool_assign(int n, int nc, int ngraph, const int64_t* batch, const int32_t* sorted_nodes,
+                    const int32_t* gstart, const int32_t* coff, int stride, int32_t* f2c,
+                    int32_t* c2f, int32_t* c2f_ptr, int64_t* cbatch, void* stream);
+int agn_pool_edge_candidates(int nc, const int32_t* c2f, const int32_t* c2f_ptr, const int32_t* rowptr,
+                             int32_t* cand_cnt, void* stream);
+int agn_pool_edge_sort(int nc, const int32_t* c2f, const int32_t* c2f_ptr, const int32_t* rowptr,
+                       const int32_t* src, const int64_t* refkey, const int32_t* f2c,
+                       const int32_t* cand_ptr, int32_t* cand_tmp, int32_t* cand_sorted,
+                       int32_t* uniq, void* stream);
+int agn_pool_edge_emit(int nc, const int32_t* cand_ptr, const int32_t* cand_sorted,
+                       const int32_t* src, const int32_t* f2c, const int32_t* crowptr,
+                       int32_t* csrc, int32_t* cdst, int32_t* cmem_ptr, int32_t* inv,
+                       int64_t* crefkey, int e_fine, void* stream);
+#ifdef __cplusplus
+}
+#endif
+#endif
