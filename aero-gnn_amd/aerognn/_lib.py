@@ -49,6 +49,18 @@ class MlpBwdArgs(C.Structure):
                 ("ln_partial", vp)]
 
 
+MAX_WGRAD = 8
+
+
+class WgradDesc(C.Structure):
+    _fields_ = [("g", vp), ("x", vp), ("ldg", i32), ("ldx", i32), ("m", i32), ("k", i32), ("rows", i32),
+                ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp)]
+
+
+class WgradBatch(C.Structure):
+    _fields_ = [("n", i32), ("_pad", i32), ("d", WgradDesc * MAX_WGRAD)]
+
+
 class PackDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
                 ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
@@ -80,6 +92,10 @@ def lib():
             "agn_mlp_bwd_nwaves": (i32, [i32]),
             "agn_mlp_backward": (i32, [C.POINTER(MlpBwdArgs), vp]),
             "agn_reduce_partials": (i32, [vp, i32, i32, vp, vp]),
+            "agn_wgrad_nsplit": (i32, [i32, i32]),
+            "agn_wgrad_partial_floats": (C.c_size_t, [i32, i32, i32]),
+            "agn_wgrad": (i32, [C.POINTER(WgradBatch), i32, i32, vp]),
+            "agn_colsum": (i32, [vp, i32, i32, vp, i32, vp, vp]),
             "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
             "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
             "agn_radix_sort_temp_bytes": (C.c_size_t, [i32]),

@@ -16,6 +16,36 @@ def stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# --------------------------------------------------------------------------- launch timing
+# When PROF is a list, every tagged kernel launch is bracketed by HIP events recorded on the
+# stream it runs on (torch's current stream): entries (tag, (alg_bytes, alg_flops), start, end).
+PROF = None
+
+
+class _Timed:
+    __slots__ = ("tag", "cost", "s")
+
+    def __init__(self, tag, cost):
+        self.tag, self.cost = tag, cost
+
+    def __enter__(self):
+        if PROF is not None and self.tag is not None:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *a):
+        if PROF is not None and self.tag is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            PROF.append((self.tag, self.cost, self.s, e))
+        return False
+
+
+def timed(tag, cost=None):
+    return _Timed(tag, cost)
+
+
 def dt_code(dtype) -> int:
     if dtype == torch.float32:
         return L.F32
@@ -124,7 +154,8 @@ class Pack:
 
 # ----------------------------------------------------------------------------- fused MLP chain
 def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out_ld=None,
-                ln=None, proj=None, src=None, dst=None, resid=None, acts=None, hpre=None, stats=None):
+                ln=None, proj=None, src=None, dst=None, resid=None, acts=None, hpre=None, stats=None,
+                tag=None, cost=None):
     """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor)."""
     a = L.MlpFwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
@@ -144,7 +175,8 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
         for i, t in enumerate(acts):
             a.act[i] = ptr(t)
     a.hpre, a.stats = ptr(hpre), ptr(stats)
-    check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
+    with timed(tag, cost):
+        check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
 
 
 def bwd_nblocks(rows):
@@ -152,7 +184,8 @@ def bwd_nblocks(rows):
 
 
 def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, gpre,
-                 ln_g=None, hpre=None, stats=None, g2=None, gidx=None, din=(), ln_partial=None):
+                 ln_g=None, hpre=None, stats=None, g2=None, gidx=None, din=(), ln_partial=None,
+                 tag=None, cost=None):
     """din: list of (k, tensor_or_None, resid_flag)."""
     a = L.MlpBwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
@@ -171,7 +204,8 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
         a.din[i] = ptr(t)
         a.din_resid[i] = int(r)
     a.ln_partial = ptr(ln_partial)
-    check(L.lib().agn_mlp_backward(C.byref(a), stream()), "mlp_backward")
+    with timed(tag, cost):
+        check(L.lib().agn_mlp_backward(C.byref(a), stream()), "mlp_backward")
 
 
 def reduce_partials(partial, nw, n, out):
@@ -192,14 +226,83 @@ def gather_rows(rows, k, idx, src, out, cnt_ptr=None, add=None):
     return out
 
 
-def wgrad(G, X, out=None):
-    """dW = G^T X accumulated in fp32 (G: [rows, M], X: [rows, K])."""
-    if G.shape[0] == 0:
-        return torch.zeros(G.shape[1], X.shape[1], dtype=torch.float32, device=G.device)
-    if G.dtype == torch.float32:
-        return torch.mm(G.t(), X, out=out) if out is not None else torch.mm(G.t(), X)
-    return torch.mm(G.t(), X, out_dtype=torch.float32)
+def colsum_rows(p, nw, n, out):
+    """out[c] = sum_r p[r][c] over nw rows, deterministic 2-level reduction (LN parameter grads)."""
+    sr = min(512, max(1, nw))
+    scratch = torch.empty(sr * n, dtype=torch.float32, device=p.device)
+    check(L.lib().agn_colsum(ptr(p), nw, n, ptr(scratch), sr, ptr(out), stream()), "colsum")
+    return out
 
 
-def colsum(G):
-    return G.sum(0, dtype=torch.float32)
+class WGrad:
+    """Batched weight/bias gradients dW = G^T X (fp32), db = colsum(G) on libaerognn.
+
+    add(G, X, dw_view, db) queues one Linear (dw_view: fp32 [M][>=K] view, may be a column
+    slice of a wider dW); run() launches ceil(n/8) kernels (+ their fixed-order reductions).
+    """
+
+    def __init__(self):
+        self.items = []
+
+    def add(self, G, X, dw, db=None):
+        assert G.dtype == X.dtype and G.shape[0] == X.shape[0]
+        assert dw.dtype == torch.float32 and dw.stride(1) == 1
+        self.items.append((G, X, dw, db))
+
+    def run(self):
+        lib = L.lib()
+        for i in range(0, len(self.items), L.MAX_WGRAD):
+            chunk = self.items[i:i + L.MAX_WGRAD]
+            rows = max(it[0].shape[0] for it in chunk)
+            dev = chunk[0][0].device
+            if rows == 0:
+                for G, X, dw, db in chunk:
+                    dw.zero_()
+                    if db is not None:
+                        db.zero_()
+                continue
+            nblk = sum(((it[0].shape[1] + 127) // 128) * ((it[1].shape[1] + 127) // 128) for it in chunk)
+            ns = int(lib.agn_wgrad_nsplit(rows, nblk))
+            sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], ns)) for G, X, _, _ in chunk]
+            bsz = [ns * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0 for G, _, _, db in chunk]
+            scratch = torch.empty(sum(sizes) + sum(bsz), dtype=torch.float32, device=dev)
+            b = L.WgradBatch()
+            b.n = len(chunk)
+            o = 0
+            for j, (G, X, dw, db) in enumerate(chunk):
+                dwp = scratch[o:o + sizes[j]]
+                o += sizes[j]
+                dbp = None
+                if db is not None:
+                    dbp = scratch[o:o + bsz[j]]
+                    o += bsz[j]
+                b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], G.shape[0],
+                                     dw.stride(0), ptr(dwp), ptr(dbp), ptr(dw), ptr(db))
+            check(lib.agn_wgrad(C.byref(b), dt_code(chunk[0][0].dtype), ns, stream()), "wgrad")
+        self.items = []
+
+
+# --------------------------------------------------------------------------- algorithmic costs
+def cost_edge_fwd(E, N, H, s, nlin, train):
+    """Minimum HBM bytes / MFMA flops of one fused edge-MLP launch."""
+    per = 2 * H * s + 8 + ((nlin - 1) * H * s + H * s + 8 if train else 0)
+    return E * per + N * 2 * H * s, 2 * E * H * H * nlin
+
+
+def cost_node_fwd(E, N, H, s, nlin, train):
+    per = 2 * H * s + 8 + ((nlin - 1) * H * s + 2 * H * s + 8 if train else 0)
+    return N * per + E * H * s, 2 * N * H * (2 * H + (nlin - 1) * H)
+
+
+def cost_proj(N, H, s):
+    return N * 3 * H * s, 2 * N * H * 2 * H
+
+
+def cost_edge_bwd(E, N, H, s, nlin):
+    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + H * s + 4
+    return E * per + N * H * s, 2 * E * H * H * nlin
+
+
+def cost_node_bwd(N, H, s, nlin):
+    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + 2 * H * s
+    return N * per, 2 * N * H * (H * (nlin - 1) + 2 * H)

@@ -15,8 +15,9 @@ from __future__ import annotations
 import torch
 
 from . import _lib as L
-from .core import (Pack, bwd_nblocks, colsum, gather_rows, mlp_backward, mlp_forward, reduce_partials,
-                   require_device, segment_sum, wgrad)
+from .core import (Pack, WGrad, bwd_nblocks, colsum_rows, cost_edge_bwd, cost_edge_fwd, cost_node_bwd,
+                   cost_node_fwd, cost_proj, gather_rows, mlp_backward, mlp_forward, require_device,
+                   segment_sum)
 
 
 def _c(t):
@@ -25,7 +26,7 @@ def _c(t):
 
 def _ln_grads(partial, nblk, M, dtype):
     out = torch.empty(2 * M, dtype=torch.float32, device=partial.device)
-    reduce_partials(partial, nblk, 2 * M, out)
+    colsum_rows(partial, nblk, 2 * M, out)
     return out[:M].to(dtype), out[M:].to(dtype)
 
 
@@ -99,25 +100,38 @@ def _alloc_saves(spec, rows, dtype, dev, train):
     return acts, hpre, stats
 
 
-def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk):
-    """Grads (in spec.params() order) from stored pre-activation grads."""
+def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk, wg=None):
+    """Grads (in spec.params() order) from stored pre-activation grads.
+
+    Queues the dW/db products on `wg` (a core.WGrad); the returned fp32 tensors are filled
+    when wg.run() executes (run here if no batch object is passed in).
+    """
+    own = wg is None
+    wg = wg or WGrad()
     grads = []
+    dev = gpre[0].device
     for l, (w, b) in enumerate(spec.linears):
         G = gpre[l]
-        if l == 0:
-            if isinstance(inputs0, (list, tuple)):
-                dw = torch.cat([wgrad(G, X) for X in inputs0], 1)
-            else:
-                dw = wgrad(G, inputs0)
+        M, K = w.shape
+        dw = torch.empty(M, K, dtype=torch.float32, device=dev)
+        db = torch.empty(M, dtype=torch.float32, device=dev) if b is not None else None
+        if l == 0 and isinstance(inputs0, (list, tuple)):
+            k0 = 0
+            for j, X in enumerate(inputs0):
+                wg.add(G, X, dw[:, k0:k0 + X.shape[1]], db if j == 0 else None)
+                k0 += X.shape[1]
         else:
-            dw = wgrad(G, acts[l - 1])
-        grads.append(dw.to(w.dtype))
+            wg.add(G, inputs0 if l == 0 else acts[l - 1], dw, db)
+        grads.append((dw, w.dtype))
         if b is not None:
-            grads.append(colsum(G).to(b.dtype))
+            grads.append((db, b.dtype))
+    if own:
+        wg.run()
+    out = [g if g.dtype == dt else g.to(dt) for g, dt in grads]
     if spec.ln is not None:
         g, bb = _ln_grads(lnp_partial, nblk, spec.out_dim, spec.ln[0].dtype)
-        grads += [g, bb]
-    return grads
+        out += [g, bb]
+    return out
 
 
 # --------------------------------------------------------------------------- MLP
@@ -271,13 +285,16 @@ class GMPFn(torch.autograd.Function):
         P = None
         if spec.trick:
             P = torch.empty(N, 2 * H, dtype=dt, device=dev)
+            sz = x.element_size()
             mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
                         segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
-                        wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P)
+                        wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
+                        tag="proj", cost=cost_proj(N, H, sz))
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
-                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est)
+                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
+                        tag="edge_fwd", cost=cost_edge_fwd(E, N, H, sz, es.nlin, train))
         else:
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None),
@@ -291,7 +308,8 @@ class GMPFn(torch.autograd.Function):
                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None),
                           (kind, H, e_out.stride(0), e_out, level.rowptr, agg)],
                     wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), resid=x, out=x_out,
-                    acts=na, hpre=nhp, stats=nst)
+                    acts=na, hpre=nhp, stats=nst,
+                    tag="node_fwd", cost=cost_node_fwd(E, N, H, x.element_size(), ns.nlin, train))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
         ctx.save_for_backward(x, e)
@@ -314,7 +332,8 @@ class GMPFn(torch.autograd.Function):
         part_n = torch.empty(nb_n, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
         mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=gx, gpre=gpre_n, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
-                     din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n)
+                     din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n,
+                     tag="node_bwd", cost=cost_node_bwd(N, H, x.element_size(), ns.nlin))
         if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
             dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
         # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
@@ -330,7 +349,8 @@ class GMPFn(torch.autograd.Function):
             din = [(H, de, True), (H, dxs, False), (H, dxd, False)]
         mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
-                     hpre=ehp, stats=est, din=din, ln_partial=part_e)
+                     hpre=ehp, stats=est, din=din, ln_partial=part_e,
+                     tag="edge_bwd", cost=cost_edge_bwd(E, N, H, x.element_size(), es.nlin))
         g0 = gpre_e[0]
         grads_edge = []
         if spec.trick:
@@ -342,8 +362,16 @@ class GMPFn(torch.autograd.Function):
                         wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
             eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e)
             eb = spec.eb
-            grads_edge = [eg[0], wgrad(dPs, x).to(eb.src_lin.dtype), wgrad(dPd, x).to(eb.dst_lin.dtype),
-                          colsum(dPd).to(eb.bias.dtype)] + eg[1:]
+            wg = WGrad()
+            dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
+            dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
+            dbd = torch.empty(H, dtype=torch.float32, device=dev)
+            wg.add(dPs, x, dws)
+            wg.add(dPd, x, dwd, dbd)
+            grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n, wg)
+            wg.run()
+            grads_edge = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
+            return (dx, de, None, None, None, *grads_edge, *grads_node)
         else:
             ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
             dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))
@@ -477,8 +505,14 @@ class EdgeBlockFn(torch.autograd.Function):
                         wpk=[spec.pack["projT"]], bias=[None], out=dx)
             eg = _chain_param_grads(es, gpre, e, ea, part, nb)
             eb = spec.eb
-            grads = [eg[0], wgrad(dPs, x).to(eb.src_lin.dtype), wgrad(dPd, x).to(eb.dst_lin.dtype),
-                     colsum(dPd).to(eb.bias.dtype)] + eg[1:]
+            wg = WGrad()
+            dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
+            dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
+            dbd = torch.empty(H, dtype=torch.float32, device=dev)
+            wg.add(dPs, x, dws)
+            wg.add(dPd, x, dwd, dbd)
+            wg.run()
+            grads = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
         else:
             ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
             dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))

@@ -1,0 +1,249 @@
+// Weight gradients dW = G^T X (and bias grads db = colsum G) for every Linear of the MLP
+// chains: G = dL/d(pre-activation) [rows x M], X = layer input [rows x K], rows = edges or
+// nodes (up to tens of millions), M, K <= 256. This is the K-reduction-over-rows half of the
+// backward of models/mlp.py / mgnLayer.py Linears (autograd's mm(grad^T, input)).
+//
+// Split-K over rows: each workgroup owns a contiguous row chunk and one 128x128 output block,
+// stages 64-row tiles of G and X in LDS (coalesced 16-B loads), and accumulates on MFMA in
+// fp32: bf16 uses v_mfma_f32_32x32x16_bf16 whose A/B operands need 8 consecutive ROWS of one
+// column -> ds_read_b64_tr_b16 transposed LDS reads; fp32 uses v_mfma_f32_32x32x2_f32 with
+// plain ds_read_b32. Per-chunk partials go to a slab and a second kernel sums the slabs in
+// fixed order: deterministic, no atomics.
+#include "common.hpp"
+#include "aerognn.h"
+
+using namespace agn;
+
+namespace {
+
+constexpr int DW_ROWS = 64;   // rows per LDS stage
+constexpr int DW_BLK = 128;   // output block edge
+constexpr int DW_THREADS = 256;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+template <typename T> struct DwTile;
+// LDS row stride in elements: bf16 136 (272 B, breaks the 4-row bank aliasing of tr reads),
+// f32 132 (528 B).
+template <> struct DwTile<bf16> { static constexpr int LD = 136; };
+template <> struct DwTile<float> { static constexpr int LD = 132; };
+
+// stage rows [r0, r0+64) x cols [c0, c0+128) of a row-major [rows][ld] matrix into LDS,
+// zero-filling out-of-range rows/cols.
+template <typename T>
+AGN_DEV void stage_tile(T* lds, const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0) {
+  constexpr int LD = DwTile<T>::LD;
+  constexpr int PER16 = 16 / sizeof(T);  // elements per 16-B chunk
+  constexpr int CHUNKS = DW_BLK / PER16; // chunks per row
+  const bool vec = ((ld % PER16) == 0) && ((c0 % PER16) == 0) && (cols - c0 >= DW_BLK);
+  for (int i = threadIdx.x; i < DW_ROWS * CHUNKS; i += DW_THREADS) {
+    const int r = i / CHUNKS, ch = i - r * CHUNKS;
+    const int gr = r0 + r;
+    T* dst = lds + r * LD + ch * PER16;
+    if (gr < rows && vec) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(g + (size_t)gr * ld + c0 + ch * PER16);
+    } else {
+#pragma unroll
+      for (int e = 0; e < PER16; ++e) {
+        const int gc = c0 + ch * PER16 + e;
+        dst[e] = (gr < rows && gc < cols) ? g[(size_t)gr * ld + gc] : from_f<T>(0.f);
+      }
+    }
+  }
+}
+
+// 8 consecutive rows (k) of one column: two ds_read_b64_tr_b16 (rows kb..kb+3, kb+4..kb+7)
+AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
+  constexpr int LD = DwTile<bf16>::LD;
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const bf16* a0 = lds + (kb + q) * LD + col_base + 4 * p;
+  const bf16* a1 = a0 + 4 * LD;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
+  bf16x8 r;
+  const bf16x4 l4 = *reinterpret_cast<const bf16x4*>(&lo);
+  const bf16x4 h4 = *reinterpret_cast<const bf16x4*>(&hi);
+  r[0] = l4[0]; r[1] = l4[1]; r[2] = l4[2]; r[3] = l4[3];
+  r[4] = h4[0]; r[5] = h4[1]; r[6] = h4[2]; r[7] = h4[3];
+  return r;
+}
+
+// grid: x = row chunk (split), y = M block * nKb + K block, z = desc
+template <typename T>
+__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
+  constexpr int LD = DwTile<T>::LD;
+  __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
+  __shared__ __attribute__((aligned(16))) T sx[DW_ROWS * LD];
+  const agn_wgrad_desc& d = b.d[blockIdx.z];
+  const int nKb = (d.k + DW_BLK - 1) / DW_BLK;
+  const int nMb = (d.m + DW_BLK - 1) / DW_BLK;
+  if ((int)blockIdx.y >= nMb * nKb) return;
+  const int mb = blockIdx.y / nKb, kb = blockIdx.y % nKb;
+  const int m0 = mb * DW_BLK, k0 = kb * DW_BLK;
+  const int split = blockIdx.x;
+  const int per = ((d.rows + nsplit - 1) / nsplit + DW_ROWS - 1) / DW_ROWS * DW_ROWS;
+  const int rbeg = split * per, rend = min(d.rows, rbeg + per);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm = (w >> 1) * 64, wk = (w & 1) * 64;  // this wave's 64x64 sub-block
+  const T* G = reinterpret_cast<const T*>(d.g);
+  const T* X = reinterpret_cast<const T*>(d.x);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+  float bsum = 0.f;  // bias colsum partial (threads 0..127 own columns m0 + tid)
+  for (int r0 = rbeg; r0 < rend; r0 += DW_ROWS) {
+    __syncthreads();
+    stage_tile<T>(sg, G, d.ldg, rend, d.m, r0, m0);
+    stage_tile<T>(sx, X, d.ldx, rend, d.k, r0, k0);
+    __syncthreads();
+    if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK) {
+#pragma unroll 8
+      for (int r = 0; r < DW_ROWS; ++r) bsum += to_f(sg[r * LD + threadIdx.x]);
+    }
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int ks = 0; ks < DW_ROWS; ks += 16) {
+        const int kbase = ks + 8 * (lane >> 5);
+        bf16x8 a[2], bb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = tr_frag(reinterpret_cast<const bf16*>(sg), kbase, wm + 32 * i + 16 * ((lane >> 4) & 1), lane);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bb[j] = tr_frag(reinterpret_cast<const bf16*>(sx), kbase, wk + 32 * j + 16 * ((lane >> 4) & 1), lane);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const float* fg = reinterpret_cast<const float*>(sg);
+      const float* fx = reinterpret_cast<const float*>(sx);
+#pragma unroll 4
+      for (int ks = 0; ks < DW_ROWS; ks += 2) {
+        const int r = ks + (lane >> 5), cidx = lane & 31;
+        float a[2], bb[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) a[i] = fg[r * LD + wm + 32 * i + cidx];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bb[j] = fx[r * LD + wk + 32 * j + cidx];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // partial slab [split][mpad][kpad] with mpad = nMb*128, kpad = nKb*128
+  const int kpad = nKb * DW_BLK;
+  float* P = d.dw_partial + (size_t)split * (nMb * DW_BLK) * kpad;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int k = k0 + wk + 32 * j + (lane & 31);
+        P[(size_t)m * kpad + k] = acc[i][j][r];
+      }
+  if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK)
+    d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum;
+}
+
+// out[m][k] = sum_s partial[s][m][k] (m < M, k < K), fixed order over s
+__global__ void wgrad_reduce_kernel(const agn_wgrad_batch b, int nsplit) {
+  const agn_wgrad_desc& d = b.d[blockIdx.y];
+  const int nKb = (d.k + DW_BLK - 1) / DW_BLK, nMb = (d.m + DW_BLK - 1) / DW_BLK;
+  const int kpad = nKb * DW_BLK, mpad = nMb * DW_BLK;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t slab = (size_t)mpad * kpad;
+  if (idx < d.m * d.k) {
+    const int m = idx / d.k, k = idx - m * d.k;
+    float s = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) s += d.dw_partial[sp * slab + (size_t)m * kpad + k];
+    d.dw[(size_t)m * d.ldw + k] = s;
+  }
+  if (d.db && idx < d.m) {
+    float s = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) s += d.db_partial[(size_t)sp * mpad + idx];
+    d.db[idx] = s;
+  }
+}
+
+// deterministic 2-level column reduction of a [nw][n] fp32 matrix
+__global__ void colsum_stage1(const float* __restrict__ p, int nw, int n, int chunk, float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r0 = blockIdx.y * chunk, r1 = min(nw, r0 + chunk);
+  if (c >= n) return;
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += p[(size_t)r * n + c];
+  part[(size_t)blockIdx.y * n + c] = s;
+}
+
+__global__ void colsum_stage2(const float* __restrict__ part, int nc, int n, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  float s = 0.f;
+  for (int r = 0; r < nc; ++r) s += part[(size_t)r * n + c];
+  out[c] = s;
+}
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
+  // ~2048 workgroups in flight over all descriptors/blocks, >= 2 LDS stages per split
+  int ns = 2048 / (ndesc_blocks > 0 ? ndesc_blocks : 1);
+  const int maxs = (rows + 2 * DW_ROWS - 1) / (2 * DW_ROWS);
+  if (ns > maxs) ns = maxs;
+  return ns < 1 ? 1 : ns;
+}
+
+size_t agn_wgrad_partial_floats(int m, int k, int nsplit) {
+  const int mp = (m + DW_BLK - 1) / DW_BLK * DW_BLK, kp = (k + DW_BLK - 1) / DW_BLK * DW_BLK;
+  return (size_t)nsplit * mp * kp;
+}
+
+int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
+  if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD || nsplit < 1) return AGN_E_ARG;
+  int maxblk = 1;
+  for (int i = 0; i < b->n; ++i) {
+    const agn_wgrad_desc& d = b->d[i];
+    if (d.m < 1 || d.k < 1 || d.rows < 0) return AGN_E_ARG;
+    const int nb = ((d.m + DW_BLK - 1) / DW_BLK) * ((d.k + DW_BLK - 1) / DW_BLK);
+    maxblk = nb > maxblk ? nb : maxblk;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid(nsplit, maxblk, b->n);
+  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
+  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
+  else return AGN_E_DTYPE;
+  int maxmk = 1;
+  for (int i = 0; i < b->n; ++i) maxmk = b->d[i].m * b->d[i].k > maxmk ? b->d[i].m * b->d[i].k : maxmk;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxmk + 255) / 256, b->n), dim3(256), 0, st, *b, nsplit);
+  return launch_status();
+}
+
+int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, float* out, void* stream) {
+  if (nw < 0 || n < 1 || scratch_rows < 1) return AGN_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (nw == 0) {
+    hipError_t e = hipMemsetAsync(out, 0, sizeof(float) * n, st);
+    return e == hipSuccess ? 0 : (int)e;
+  }
+  const int chunk = (nw + scratch_rows - 1) / scratch_rows;
+  const int nc = (nw + chunk - 1) / chunk;
+  hipLaunchKernelGGL(colsum_stage1, dim3((n + 255) / 256, nc), dim3(256), 0, st, p, nw, n, chunk, scratch);
+  hipLaunchKernelGGL(colsum_stage2, dim3((n + 255) / 256), dim3(256), 0, st, scratch, nc, n, out);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""Throughput benchmark: million edge-updates/s of the BSMS-MGN training step on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): BiStridedMeshGraphNet, 4 scales, 2 layers per
+scale, stride 2, processor_size 15, H=128, n_hid=2 everywhere, do_concat_trick=True, on a
+synthetic 1,000,000-node / 5,996,000-edge ellipsoid aero surface mesh; bf16 activations,
+fp32 master weights, Adam. One step = forward (incl. the per-forward pooling hierarchy
+build, as the reference does) + MSE + backward + gradient all-reduce + Adam.
+An edge-update is one directed edge processed by one MeshGraphNetLayer;
+EU/step is counted from the actual hierarchy (82,432,142 for C3).
+
+N GPUs (torchrun): every rank trains on its own mesh of the same size (rotation seed = rank),
+one RCCL gradient all-reduce per step: weak scaling, value = total EU / max-rank time.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "aero-gnn_amd"))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("AEROGNN_MEMLOG", "0")
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+MFMA_PEAK = {"bf16": 2500.0, "f32": 157.3}   # dense TFLOP/s (spec; no sparsity)
+
+CONFIGS = {
+    # name: (nu, nv, num_scales, dtype)
+    "c3": (1000, 1000, 4, torch.bfloat16),
+    "c2": (400, 250, 1, torch.float32),
+    "c5": (2500, 2000, 6, torch.bfloat16),
+    "small": (200, 125, 4, torch.bfloat16),
+}
+
+
+def build_model(num_scales, dev):
+    from models.bsms_mgn import BiStridedMeshGraphNet
+    kw = dict(processor_size=15, activation_fn="relu", num_hidden_layers_node_processor=2,
+              num_hidden_layers_edge_processor=2, hidden_dim_processor=128, num_hidden_layers_node_encoder=2,
+              hidden_dim_node_encoder=128, num_hidden_layers_edge_encoder=2, hidden_dim_edge_encoder=128,
+              aggregation="add", hidden_dim_decoder=128, num_hidden_layers_decoder=2, dropout=0.0,
+              do_concat_trick=True, num_scales=num_scales, layers_per_scale=2, stride=2)
+    torch.manual_seed(0)
+    return BiStridedMeshGraphNet(6, 4, 4, **kw).to(dev), kw
+
+
+def mesh_tensors(nu, nv, seed, dev, dtype):
+    from aerognn.meshgen import ellipsoid
+    m = ellipsoid(nu, nv, seed=seed)
+    t = {k: torch.from_numpy(v).to(dev) for k, v in m.items()}
+    for k in ("x", "edge_attr"):
+        t[k] = t[k].to(dtype)
+    return t
+
+
+def edge_updates(model, t):
+    """EU per step = sum over processor layers of the edge count of the level it runs on."""
+    level, pools = model._hierarchy(t["edge_index"], None, t["pos"], t["x"].shape[0])
+    E = [level.E] + [p.coarse.E for p in pools]
+    nd = len(model.down_layers)
+    eu = sum(len(model.down_layers[s]) * E[s] for s in range(nd))
+    eu += len(model.bottleneck_layers) * E[nd]
+    eu += sum(len(model.up_layers[s]) * E[nd - 1 - s] for s in range(nd))
+    return eu, E
+
+
+def cpu_baseline(num_scales, seconds_hint=20.0):
+    """Oracle (oracle/refcpu.py, op-for-op the reference's CPU path) timed on host cores:
+    one fp32 training step (fwd + MSE + bwd) of the same model on a bounded sample mesh."""
+    from aerognn.meshgen import ellipsoid
+    from oracle import refcpu as R
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    nu, nv = 250, 200  # 50,000 nodes / 299,000 edges
+    m = ellipsoid(nu, nv, seed=0)
+    t = {k: torch.from_numpy(v) for k, v in m.items()}
+    model, kw = build_model(num_scales, "cpu")
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    cfg = R.cfg_from_kwargs(**kw)
+    batch = torch.zeros(t["x"].shape[0], dtype=torch.long)
+    # EU of the sample
+    down, bott, up = R.bsms_schedule(cfg["processor_size"], cfg["num_scales"], cfg["layers_per_scale"])
+    Es, ei, pos, b = [], t["edge_index"], t["pos"], batch
+    Es.append(ei.shape[1])
+    node = torch.zeros(t["x"].shape[0], 1)
+    for _ in down:
+        node, _e, ei, b, pos, _a = R.downsample(node, torch.zeros(ei.shape[1], 1), ei, b, pos, cfg["stride"], True)
+        Es.append(ei.shape[1])
+    eu = sum(c * Es[i] for i, c in enumerate(down)) + bott * Es[len(down)] + \
+        sum(c * Es[len(down) - 1 - i] for i, c in enumerate(up))
+    t0 = time.perf_counter()
+    pred = R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch, t["pos"], stable=True)
+    loss = torch.nn.functional.mse_loss(pred, t["y"])
+    loss.backward()
+    dt = time.perf_counter() - t0
+    return {"value": eu / dt / 1e6, "unit": "M edge-updates/s", "cores": nthreads, "kind": "port",
+            "sample": f"1 fp32 train step (fwd+MSE+bwd) of the same BSMS-{num_scales} model, oracle/refcpu.py "
+                      f"(the reference's aten ops in order) on a {nu * nv}-node/{m['edge_index'].shape[1]}-edge "
+                      f"ellipsoid, {eu} EU, {dt:.1f} s, torch threads={nthreads}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--mode", default="train", choices=["train", "fwd"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    args = ap.parse_args()
+
+    from aerognn import core, dist as D
+    rank, ws = D.init_from_env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    nu, nv, S, dtype = CONFIGS[args.config]
+
+    model, kw = build_model(S, dev)
+    t = mesh_tensors(nu, nv, seed=rank, dev=dev, dtype=dtype)
+    eu_step, Es = edge_updates(model, t)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    allreduce = D.GradAllReduce(model.parameters())
+    n_glob = D.global_count(t["y"].numel(), dev)
+
+    def step():
+        if args.mode == "train":
+            pred = model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"])
+            loss = D.mse_sum_loss(pred, t["y"], n_glob)
+            loss.backward()
+            allreduce()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+        else:
+            with torch.no_grad():
+                model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    core.PROF = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if ws > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    prof, core.PROF = core.PROF, None
+    if ws > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    # per-kernel device time from the HIP events recorded on the launch stream
+    agg = {}
+    for tag, cost, s, e in prof:
+        ms = s.elapsed_time(e)
+        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += ms
+        a[2] += cost[0] if cost else 0.0
+        a[3] += cost[1] if cost else 0.0
+    dom = max(agg.items(), key=lambda kv: kv[1][1]) if agg else None
+    roof = None
+    kernels = {}
+    for tag, (n, ms, by, fl) in agg.items():
+        kernels[tag] = {"launches": n, "avg_us": 1e3 * ms / n, "alg_GBs": by / (ms * 1e-3) / 1e9,
+                        "alg_TFLOPs": fl / (ms * 1e-3) / 1e12, "share_of_step": ms / (1e3 * elapsed)}
+    dname = "bf16" if dtype == torch.bfloat16 else "f32"
+    if dom:
+        tag, (n, ms, by, fl) = dom
+        ach = by / n / (ms / n * 1e-3) / 1e9
+        traffic = None
+        if args.traffic and os.path.exists(args.traffic):
+            traffic = json.load(open(args.traffic)).get(tag)
+        roof = {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "alg_bytes_per_launch": by / n, "avg_launch_us": 1e3 * ms / n,
+                "mfma_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "mfma_peak": MFMA_PEAK[dname]}
+
+    value = eu_step * args.steps * ws / elapsed / 1e6
+    out = {
+        "metric": "million edge-updates/sec, 1M-node/6M-edge mesh, 1->8 MI355X",
+        "value": round(value, 2),
+        "unit": "M edge-updates/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dname,
+        "data": "synthetic ellipsoid aero surface mesh (aerognn.meshgen), random-init weights (seed 0)",
+        "config": {"workload": f"BSMS-MGN {S}-scale U-Net train step (fwd+MSE+bwd+allreduce+Adam), "
+                               f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU",
+                   "model": "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)",
+                   "mode": args.mode, "edge_updates_per_step_per_gpu": eu_step, "level_edges": Es,
+                   "global_batch": ws, "parallelism": f"dp{ws}"},
+        "roofline": roof,
+        "kernels": kernels,
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(S)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

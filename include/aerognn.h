@@ -23,6 +23,7 @@
  *                     :280 torch.unique(keys) ordering; CSC/CSR construction for aggregation
  *   agn_pool_*        bsms_mgn.py:217-301 (_downsample: index map, coarse edge coalesce, means)
  *   agn_pack          layout conversion of nn.Linear weights into MFMA A-fragments
+ *   agn_wgrad         weight / bias gradients of every Linear (mm(grad^T, input) in autograd)
  */
 #ifndef AEROGNN_H
 #define AEROGNN_H
@@ -125,6 +126,31 @@ typedef struct {
   int dst_rows;
   int dst_cols;
 } agn_pack_desc;
+
+/* ---- weight gradients: dW = G^T X, db = colsum(G) (autograd of every nn.Linear on the path:
+ * mlp.py:42-46, mgnLayer.py:97-99 / :147-149, :127-132) ---- */
+#define AGN_MAX_WGRAD 8
+typedef struct {
+  const void* g;        /* [rows][m] pre-activation grads (activation dtype) */
+  const void* x;        /* [rows][k] layer input */
+  int ldg, ldx;         /* row strides (elements) */
+  int m, k, rows;
+  int ldw;              /* row stride of dw (floats) */
+  float* dw_partial;    /* agn_wgrad_partial_floats(m, k, nsplit) scratch */
+  float* db_partial;    /* nsplit * round_up(m, 128) scratch, or NULL (no bias) */
+  float* dw;            /* [m][ldw] fp32 output */
+  float* db;            /* [m] fp32 output or NULL */
+} agn_wgrad_desc;
+typedef struct {
+  int n;
+  int _pad;
+  agn_wgrad_desc d[AGN_MAX_WGRAD];
+} agn_wgrad_batch;
+int agn_wgrad_nsplit(int rows, int ndesc_blocks);
+size_t agn_wgrad_partial_floats(int m, int k, int nsplit);
+int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream);
+/* out[c] = sum_r p[r][c] (r < nw, c < n) in fixed order via scratch[scratch_rows][n] */
+int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, float* out, void* stream);
 
 int agn_version(void);
 const char* agn_error_string(int code);
