@@ -119,6 +119,24 @@ template <int NR> struct BOp<bf16, NR> {
     bf16x8 a = *reinterpret_cast<const bf16x8*>(&a_raw);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, u[unit], acc, 0, 0, 0);
   }
+  // relu(acc) straight into the packed operand (register rho = 16*t + r of acc tile t)
+  template <int NT>
+  AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[i][j] = (bf16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
+  }
+  // store the packed activations as a row of `H` bf16 (two 4-feature chunks per unit)
+  AGN_DEV void store(bf16* rowp, int h) const {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      const bf16x4 lo = {u[i][0], u[i][1], u[i][2], u[i][3]};
+      const bf16x4 hi = {u[i][4], u[i][5], u[i][6], u[i][7]};
+      *reinterpret_cast<bf16x4*>(rowp + 16 * i + 4 * h) = lo;
+      *reinterpret_cast<bf16x4*>(rowp + 16 * i + 8 + 4 * h) = hi;
+    }
+  }
 };
 template <int NR> struct BOp<float, NR> {
   static constexpr int RPU = 4;
@@ -131,6 +149,16 @@ template <int NR> struct BOp<float, NR> {
     f32x4 a = *reinterpret_cast<const f32x4*>(&a_raw);
 #pragma unroll
     for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[e], u[4 * unit + e], acc, 0, 0, 0);
+  }
+  template <int NT>
+  AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) u[i] = fmaxf(acc[i / 16][i % 16], 0.f);
+  }
+  AGN_DEV void store(float* rowp, int h) const {
+#pragma unroll
+    for (int q = 0; q < NR / 4; ++q)
+      *reinterpret_cast<f32x4*>(rowp + 8 * q + 4 * h) = f32x4{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]};
   }
 };
 
@@ -172,28 +200,32 @@ AGN_DEV float xor32(float v) { return __shfl_xor(v, 32, 64); }
 // Transpose-reduce NR per-lane values over the 32 lanes of each half (lanes c = l & 31).
 // On return lane c holds in v[i] (i < max(NR/32,1)) the 32-lane sum of register
 // rho = floor(c*NR/32) + i; for NR < 32 the 32/NR lanes sharing a rho hold identical sums.
-template <int NR>
-AGN_DEV void butterfly_reduce(float (&v)[NR], int lane) {
-  const int c = lane & 31;
-  int n = NR;
+template <int NR, int N, int M>
+struct Butterfly {
+  // one exchange step: keep half of the N live registers, add the partner's other half
+  static AGN_DEV void run(float (&v)[NR], int c) {
+    if constexpr (M >= 1) {
+      if constexpr (N >= 2) {
+        constexpr int HALF = N / 2;
+        const bool upper = (c & M) != 0;
 #pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) {
-    if (n >= 2) {
-      const bool upper = (c & m) != 0;
-      const int half = n / 2;
-#pragma unroll
-      for (int i = 0; i < NR / 2; ++i) {
-        if (i < half) {
-          float keep = upper ? v[half + i] : v[i];
-          float send = upper ? v[i] : v[half + i];
-          v[i] = keep + __shfl_xor(send, m, 64);
+        for (int i = 0; i < HALF; ++i) {
+          const float keep = upper ? v[HALF + i] : v[i];
+          const float send = upper ? v[i] : v[HALF + i];
+          v[i] = keep + __shfl_xor(send, M, 64);
         }
+        Butterfly<NR, HALF, M / 2>::run(v, c);
+      } else {
+        v[0] += __shfl_xor(v[0], M, 64);
+        Butterfly<NR, 1, M / 2>::run(v, c);
       }
-      n = half;
-    } else {
-      v[0] += __shfl_xor(v[0], m, 64);
     }
   }
+};
+
+template <int NR>
+AGN_DEV void butterfly_reduce(float (&v)[NR], int lane) {
+  Butterfly<NR, NR, 16>::run(v, lane & 31);
 }
 
 }  // namespace agn

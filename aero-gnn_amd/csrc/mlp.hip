@@ -112,7 +112,7 @@ AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid,
 
 // ------------------------------------------------------------------------- forward
 template <typename T, int NT, bool VEC>
-__global__ __launch_bounds__(BLOCK) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
+__global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;  // K units of an H-wide input
@@ -143,8 +143,10 @@ __global__ __launch_bounds__(BLOCK) void mlp_fwd_kernel(const agn_mlp_fwd_args a
       const T* P = reinterpret_cast<const T*>(a.proj);
       const T* ps = P + (size_t)a.src[rr] * (2 * H);
       const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
+      // one 32-feature tile per round: keeps the gathered rows from all being live at once
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+      for (int t = 0; t < NT; ++t) {
+        cbarrier();
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int f0 = 32 * t + 8 * q + 4 * h;
@@ -152,6 +154,7 @@ __global__ __launch_bounds__(BLOCK) void mlp_fwd_kernel(const agn_mlp_fwd_args a
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = x[e] + y[e];
         }
+      }
     } else {
       acc_bias<NT, VEC>(acc, a.bias[0] ? a.bias[0] + gofs : nullptr, nv0, h);
     }
@@ -168,60 +171,76 @@ __global__ __launch_bounds__(BLOCK) void mlp_fwd_kernel(const agn_mlp_fwd_args a
       else gemm<T, NT, NR>(acc, b, nu, wl, nu, otn0, lane);
       unit += nu;
     }
-    // ---- hidden layers
+    // ---- hidden layers: relu(acc) -> packed operand -> next Linear (registers only)
     for (int l = 1; l < a.nlin; ++l) {
       const int outl = (l == a.nlin - 1) ? a.out_dim : H;
       const int otn = (outl + 31) / 32;
       __syncthreads();
       stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
-      acc_to_regs<NT, NR>(v, acc);
-#pragma unroll
-      for (int i = 0; i < NR; ++i) v[i] = fmaxf(v[i], 0.f);
-      if (a.act[l - 1] && valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, H, v, h);
-      b.set(v);
-      cbarrier();
+      b.template set_relu<NT>(acc);
+      if (a.act[l - 1] && valid) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h);
       acc_bias<NT, VEC>(acc, a.bias[l], outl, h);
       __syncthreads();
       if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
       else gemm<T, NT, NR>(acc, b, NUH, wl, NUH, otn, lane);
     }
-    // ---- epilogue: LayerNorm, residual, store
-    cbarrier();
+    // ---- epilogue: LayerNorm, residual, store (in place on the accumulators, 4 features at a time)
     const int outd = (a.nlin == 1) ? nv0 : a.out_dim;
-    acc_to_regs<NT, NR>(v, acc);
+    float mean = 0.f, rstd = 1.f;
     if (a.use_ln) {
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) s += (VEC || feat_of(i, h) < outd) ? v[i] : 0.f;
+      for (int i = 0; i < NR; ++i) s += (VEC || feat_of(i, h) < outd) ? acc[i / 16][i % 16] : 0.f;
       s += xor32(s);
-      const float mean = s / (float)outd;
+      mean = s / (float)outd;
       float q = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
-        const float d = v[i] - mean;
+        const float d = acc[i / 16][i % 16] - mean;
         q += (VEC || feat_of(i, h) < outd) ? d * d : 0.f;
       }
       q += xor32(q);
-      const float rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
-      if (a.hpre && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.hpre) + (size_t)row * outd, outd, v, h);
+      rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
       if (a.stats && valid && h == 0) {
         a.stats[2 * (size_t)row] = mean;
         a.stats[2 * (size_t)row + 1] = rstd;
       }
-float lg[NR], lb[NR];
-      load_param<NR, VEC>(lg, a.ln_g, outd, h);
-      load_param<NR, VEC>(lb, a.ln_b, outd, h);
-#pragma unroll
-      for (int i = 0; i < NR; ++i) v[i] = (v[i] - mean) * rstd * lg[i] + lb[i];
     }
-    if (a.resid) {
-      cbarrier();
-      float r[NR];
-      load_row<T, NR, VEC>(r, reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs, outd, h);
+    T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * outd : nullptr;
+    const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs : nullptr;
+    T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) v[i] = round_t<T>(v[i]) + r[i];
+    for (int q = 0; q < NR / 4; ++q) {
+      const int f0 = 8 * q + 4 * h;
+      f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
+                 acc[q / 4][4 * (q % 4) + 3]};
+      if (a.use_ln) {
+        if (hp && valid) {
+          if (VEC) store4(hp + f0, v);
+          else store4_masked(hp, f0, outd, false, v);
+        }
+        f32x4 g4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
+        if (VEC) {
+          g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+          b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (f0 + e < outd) { g4[e] = a.ln_g[f0 + e]; b4[e] = a.ln_b[f0 + e]; }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
+      }
+      if (rp) {
+        const f32x4 r = VEC ? load4(rp + f0) : load4_masked(rp, f0, outd, false);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = round_t<T>(v[e]) + r[e];
+      }
+      if (valid) {
+        if (VEC) store4(op + f0, v);
+        else store4_masked(op, f0, outd, false, v);
+      }
     }
-    if (valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs, outd, v, h);
   }
 }
 
@@ -239,7 +258,7 @@ AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool v
 }
 
 template <typename T, int NT, bool VEC>
-__global__ __launch_bounds__(BLOCK) void mlp_bwd_kernel(const agn_mlp_bwd_args a) {
+__global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NP = (NR >= 32) ? NR / 32 : 1;
@@ -257,29 +276,37 @@ __global__ __launch_bounds__(BLOCK) void mlp_bwd_kernel(const agn_mlp_bwd_args a
   float A[NR];  // current dL/d(pre-activation)
   load_grad<T, NR, VEC>(A, a, rr, valid, h);
   if (a.use_ln) {
+    // LayerNorm backward, streamed 4 features at a time (hpre, gamma re-read per chunk)
     const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
     const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * M;
     float B[NR];
-    load_row<T, NR, VEC>(B, hp, M, h);
     float c1 = 0.f, c2 = 0.f;
-    float lg[NR];
-    load_param<NR, VEC>(lg, a.ln_g, M, h);
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int f = feat_of(i, h);
-      const bool in = VEC || f < M;
-      B[i] = in ? (B[i] - mean) * rstd : 0.f;
-      const float gg = A[i] * lg[i];
-      c1 += gg;
-      c2 += gg * B[i];
+    for (int q = 0; q < NR / 4; ++q) {
+      const int f0 = 8 * q + 4 * h;
+      const f32x4 hv = VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
+      f32x4 gm = {0.f, 0.f, 0.f, 0.f};
+      if (VEC) gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+      else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (f0 + e < M) gm[e] = a.ln_g[f0 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = VEC || f0 + e < M;
+        const float xh = in ? (hv[e] - mean) * rstd : 0.f;
+        const float gg = A[4 * q + e] * gm[e];
+        c1 += gg;
+        c2 += gg * xh;
+        B[4 * q + e] = A[4 * q + e] * xh;  // g * xhat (LN weight-grad partial)
+      }
     }
     c1 += xor32(c1);
     c2 += xor32(c2);
     c1 /= (float)M;
     c2 /= (float)M;
     if (a.ln_partial) {  // LayerNorm parameter partials over the wave's 32 rows (butterfly)
-#pragma unroll
-      for (int i = 0; i < NR; ++i) B[i] *= A[i];
       butterfly_reduce<NR>(B, lane);
       float pg[NP];
 #pragma unroll
@@ -293,14 +320,24 @@ __global__ __launch_bounds__(BLOCK) void mlp_bwd_kernel(const agn_mlp_bwd_args a
         const int f = feat_of((c * NR) / 32 + i, h);
         if (canon) { lnp[wid][0][f] = pg[i]; lnp[wid][1][f] = B[i]; }
       }
-      load_row<T, NR, VEC>(B, hp, M, h);
-#pragma unroll
-      for (int i = 0; i < NR; ++i) B[i] = (B[i] - mean) * rstd;
     }
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const int f = feat_of(i, h);
-      A[i] = (VEC || f < M) ? (A[i] * lg[i] - c1 - B[i] * c2) * rstd : 0.f;
+    for (int q = 0; q < NR / 4; ++q) {
+      const int f0 = 8 * q + 4 * h;
+      const f32x4 hv = VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
+      f32x4 gm = {0.f, 0.f, 0.f, 0.f};
+      if (VEC) gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+      else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (f0 + e < M) gm[e] = a.ln_g[f0 + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = VEC || f0 + e < M;
+        const float xh = (hv[e] - mean) * rstd;
+        A[4 * q + e] = in ? (A[4 * q + e] * gm[e] - c1 - xh * c2) * rstd : 0.f;
+      }
     }
   }
   // chain rule through the Linear / ReLU stack
