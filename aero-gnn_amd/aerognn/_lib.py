@@ -39,7 +39,7 @@ class MlpFwdArgs(C.Structure):
 
 class MlpBwdArgs(C.Structure):
     _fields_ = [("rows", i32), ("dtype", i32), ("hidden", i32), ("nlin", i32),
-                ("out_dim", i32), ("in_dim", i32), ("use_ln", i32), ("_unused", i32),
+                ("out_dim", i32), ("in_dim", i32), ("use_ln", i32), ("ln_rows", i32),
                 ("wtpk", vp * MAX_LIN), ("act", vp * MAX_LIN),
                 ("hpre", vp), ("stats", vp), ("ln_g", vp),
                 ("g", vp), ("g2", vp), ("gidx", vp),
@@ -102,7 +102,8 @@ def lib():
             "agn_radix_sort_u64": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
             "agn_row_ptr": (i32, [vp, i32, i32, vp, vp]),
             "agn_row_ptr_i64": (i32, [vp, i32, i32, vp, vp]),
-            "agn_exclusive_scan_i32": (i32, [vp, vp, i32, vp, vp]),
+            "agn_scan_temp_bytes": (C.c_size_t, [i32]),
+            "agn_exclusive_scan_i32": (i32, [vp, vp, i32, vp, vp, vp]),
             "agn_pool_sort_keys": (i32, [i32, vp, vp, i32, vp, vp, vp]),
             "agn_pool_assign": (i32, [i32, i32, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp]),
             "agn_pool_edge_candidates": (i32, [i32, vp, vp, vp, vp, vp]),

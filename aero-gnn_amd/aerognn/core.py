@@ -206,6 +206,7 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
     a.ln_partial = ptr(ln_partial)
     with timed(tag, cost):
         check(L.lib().agn_mlp_backward(C.byref(a), stream()), "mlp_backward")
+    return a.ln_rows
 
 
 def reduce_partials(partial, nw, n, out):

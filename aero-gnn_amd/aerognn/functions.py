@@ -181,7 +181,7 @@ class MLPFn(torch.autograd.Function):
                   for _, k in ks]
         nblk = bwd_nblocks(rows)
         part = torch.empty(nblk, 2 * spec.out_dim, dtype=torch.float32, device=x.device) if spec.ln else None
-        mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+        nblk = mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
                      in_dim=spec.in_dim, wtpk=spec.wtpk(), acts=ctx.acts or [], g=gy, gpre=gpre,
                      ln_g=spec.lnp()[0] if spec.ln else None, hpre=ctx.hpre, stats=ctx.stats,
                      din=[(k, d, False) for (_, k), d in zip(ks, dparts)], ln_partial=part)
@@ -330,7 +330,7 @@ class GMPFn(torch.autograd.Function):
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb_n = bwd_nblocks(N)
         part_n = torch.empty(nb_n, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
-        mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+        nb_n = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=gx, gpre=gpre_n, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
                      din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n,
                      tag="node_bwd", cost=cost_node_bwd(N, H, x.element_size(), ns.nlin))
@@ -347,7 +347,7 @@ class GMPFn(torch.autograd.Function):
             dxs = torch.empty(E, H, dtype=dt, device=dev)
             dxd = torch.empty(E, H, dtype=dt, device=dev)
             din = [(H, de, True), (H, dxs, False), (H, dxd, False)]
-        mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
+        nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
                      hpre=ehp, stats=est, din=din, ln_partial=part_e,
                      tag="edge_bwd", cost=cost_edge_bwd(E, N, H, x.element_size(), es.nlin))
@@ -492,7 +492,7 @@ class EdgeBlockFn(torch.autograd.Function):
             dxs = torch.empty(E, H, dtype=dt, device=dev)
             dxd = torch.empty(E, H, dtype=dt, device=dev)
             din = [(H, de, False), (H, dxs, False), (H, dxd, False)]
-        mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
+        nb = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=g, gpre=gpre, ln_g=es.lnp()[0] if es.ln else None, hpre=ehp, stats=est,
                      din=din, ln_partial=part)
         if spec.trick:
@@ -559,7 +559,7 @@ class NodeBlockFn(torch.autograd.Function):
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb = bwd_nblocks(N)
         part = torch.empty(nb, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
-        mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+        nb = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=g, gpre=gpre, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
                      din=[(H, dx, False), (H, dagg, False)], ln_partial=part)
         de = torch.empty_like(e)

@@ -50,7 +50,9 @@ def group_by(keys_i32: torch.Tensor, nrows: int):
 
 def exclusive_scan(x: torch.Tensor):
     out = torch.empty(x.numel() + 1, dtype=I32, device=x.device)
-    check(L.lib().agn_exclusive_scan_i32(ptr(x), ptr(out), x.numel(), ptr(out[x.numel():]), stream()), "scan")
+    scr = torch.empty(int(L.lib().agn_scan_temp_bytes(x.numel())) // 4 + 1, dtype=I32, device=x.device)
+    check(L.lib().agn_exclusive_scan_i32(ptr(x), ptr(out), x.numel(), ptr(out[x.numel():]), ptr(scr), stream()),
+          "scan")
     return out
 
 

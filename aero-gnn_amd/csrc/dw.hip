@@ -152,18 +152,27 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum;
 }
 
-// out[m][k] = sum_s partial[s][m][k] (m < M, k < K), fixed order over s
+// out[m][k] = sum_s partial[s][m][k] (m < M, k < K), fixed order over s; 4 columns per thread
 __global__ void wgrad_reduce_kernel(const agn_wgrad_batch b, int nsplit) {
   const agn_wgrad_desc& d = b.d[blockIdx.y];
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK, nMb = (d.m + DW_BLK - 1) / DW_BLK;
   const int kpad = nKb * DW_BLK, mpad = nMb * DW_BLK;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over m * kpad / 4
   const size_t slab = (size_t)mpad * kpad;
-  if (idx < d.m * d.k) {
-    const int m = idx / d.k, k = idx - m * d.k;
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += d.dw_partial[sp * slab + (size_t)m * kpad + k];
-    d.dw[(size_t)m * d.ldw + k] = s;
+  const int kq = kpad / 4;
+  if (idx < d.m * kq) {
+    const int m = idx / kq, k0 = 4 * (idx - m * kq);
+    if (k0 < d.k) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+      const float* p = d.dw_partial + (size_t)m * kpad + k0;
+      for (int sp = 0; sp < nsplit; ++sp) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(p + sp * slab);
+        s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (k0 + e < d.k) d.dw[(size_t)m * d.ldw + k0 + e] = s[e];
+    }
   }
   if (d.db && idx < d.m) {
     float s = 0.f;
@@ -201,7 +210,7 @@ extern "C" {
 
 int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
   // ~2048 workgroups in flight over all descriptors/blocks, >= 2 LDS stages per split
-  int ns = 2048 / (ndesc_blocks > 0 ? ndesc_blocks : 1);
+  int ns = 1024 / (ndesc_blocks > 0 ? ndesc_blocks : 1);
   const int maxs = (rows + 2 * DW_ROWS - 1) / (2 * DW_ROWS);
   if (ns > maxs) ns = maxs;
   return ns < 1 ? 1 : ns;
@@ -227,7 +236,11 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
   else return AGN_E_DTYPE;
   int maxmk = 1;
-  for (int i = 0; i < b->n; ++i) maxmk = b->d[i].m * b->d[i].k > maxmk ? b->d[i].m * b->d[i].k : maxmk;
+  for (int i = 0; i < b->n; ++i) {
+    const int kq = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK / 4;
+    const int v = b->d[i].m * kq > b->d[i].m ? b->d[i].m * kq : b->d[i].m;
+    maxmk = v > maxmk ? v : maxmk;
+  }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxmk + 255) / 256, b->n), dim3(256), 0, st, *b, nsplit);
   return launch_status();
 }

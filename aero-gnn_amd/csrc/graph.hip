@@ -117,6 +117,80 @@ __global__ __launch_bounds__(1024) void scan_single_kernel(const int32_t* __rest
   if (t == 1023 && total) *total = part[1023];
 }
 
+// ---- 3-phase exclusive scan (int32): block sums -> scan of block sums -> block-local scan + offset
+constexpr int SC_THREADS = 256;
+constexpr int SC_ITEMS = 16;
+constexpr int SC_TILE = SC_THREADS * SC_ITEMS;
+
+__global__ __launch_bounds__(SC_THREADS) void scan_bsum_kernel(const int32_t* __restrict__ in, int n,
+                                                              int32_t* __restrict__ bsum) {
+  __shared__ int32_t red[SC_THREADS];
+  const int base = blockIdx.x * SC_TILE;
+  int32_t s = 0;
+  for (int i = threadIdx.x; i < SC_TILE; i += SC_THREADS) {
+    const int p = base + i;
+    if (p < n) s += in[p];
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = SC_THREADS / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(SC_THREADS) void scan_tile_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                              int n, const int32_t* __restrict__ boff) {
+  __shared__ int32_t buf[SC_TILE];
+  __shared__ int32_t part[SC_THREADS];
+  const int base = blockIdx.x * SC_TILE;
+  for (int i = threadIdx.x; i < SC_TILE; i += SC_THREADS) {
+    const int p = base + i;
+    buf[i] = p < n ? in[p] : 0;
+  }
+  __syncthreads();
+  int32_t s = 0;
+  const int t0 = threadIdx.x * SC_ITEMS;
+#pragma unroll
+  for (int j = 0; j < SC_ITEMS; ++j) s += buf[t0 + j];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < SC_THREADS; off <<= 1) {
+    const int32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int32_t run = (threadIdx.x == 0 ? 0 : part[threadIdx.x - 1]) + (boff ? boff[blockIdx.x] : 0);
+#pragma unroll
+  for (int j = 0; j < SC_ITEMS; ++j) {
+    const int32_t v = buf[t0 + j];
+    buf[t0 + j] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < SC_TILE; i += SC_THREADS) {
+    const int p = base + i;
+    if (p < n) out[p] = buf[i];
+  }
+}
+
+// exclusive scan with scratch of (nb + 1) ints, nb = ceil(n / SC_TILE); total (optional) = sum
+int scan_launch(const int32_t* in, int32_t* out, int n, int32_t* total, int32_t* scratch, hipStream_t st) {
+  const int nb = (n + SC_TILE - 1) / SC_TILE;
+  if (nb <= 1) {
+    hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, in, out, n, total);
+    return 0;
+  }
+  int32_t* bsum = scratch;
+  int32_t* boff = scratch + nb;
+  hipLaunchKernelGGL(scan_bsum_kernel, dim3(nb), dim3(SC_THREADS), 0, st, in, n, bsum);
+  hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, bsum, boff, nb, total);
+  hipLaunchKernelGGL(scan_tile_kernel, dim3(nb), dim3(SC_THREADS), 0, st, in, out, n, boff);
+  return 0;
+}
+
 __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint64_t* __restrict__ keys_in,
                                                                 const int32_t* __restrict__ vals_in, int n,
                                                                 int shift, int nblocks,
@@ -381,7 +455,8 @@ int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* 
 
 size_t agn_radix_sort_temp_bytes(int n) {
   const int nb = (n + RS_TILE - 1) / RS_TILE;
-  return (size_t)2 * 256 * (nb > 0 ? nb : 1) * sizeof(int32_t) + 256;
+  const int m = 256 * (nb > 0 ? nb : 1);
+  return (size_t)(2 * m + 2 * ((m + SC_TILE - 1) / SC_TILE) + 2) * sizeof(int32_t) + 256;
 }
 
 int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t* keys_tmp, int32_t* vals_tmp,
@@ -392,13 +467,14 @@ int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t*
   const int nb = (n + RS_TILE - 1) / RS_TILE;
   int32_t* counts = reinterpret_cast<int32_t*>(scratch);
   int32_t* offs = counts + 256 * nb;
+  int32_t* sscr = offs + 256 * nb;
   uint64_t *ki = keys, *ko = keys_tmp;
   int32_t *vi = vals, *vo = vals_tmp;
   const int passes = (bits + 7) / 8;
   for (int p = 0; p < passes; ++p) {
     const int shift = 8 * p;
     hipLaunchKernelGGL(rs_hist_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, n, shift, nb, counts);
-    hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, counts, offs, 256 * nb, (int32_t*)nullptr);
+    scan_launch(counts, offs, 256 * nb, (int32_t*)nullptr, sscr, st);
     hipLaunchKernelGGL(rs_scatter_kernel, dim3(nb), dim3(RS_THREADS), 0, st, ki, vi, n, shift, nb, offs, ko, vo);
     std::swap(ki, ko);
     std::swap(vi, vo);
@@ -412,7 +488,11 @@ int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t*
   return launch_status();
 }
 
-int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, void* stream) {
+size_t agn_scan_temp_bytes(int n) {
+  return (size_t)(2 * ((n + SC_TILE - 1) / SC_TILE) + 2) * sizeof(int32_t);
+}
+
+int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, int32_t* scratch, void* stream) {
   if (n < 0) return AGN_E_ARG;
   hipStream_t st = (hipStream_t)stream;
   if (n == 0) {
@@ -422,7 +502,7 @@ int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* tota
     }
     return launch_status();
   }
-  hipLaunchKernelGGL(scan_single_kernel, dim3(1), dim3(1024), 0, st, in, out, n, total);
+  scan_launch(in, out, n, total, scratch, st);
   return launch_status();
 }
 

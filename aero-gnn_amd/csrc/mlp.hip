@@ -404,6 +404,229 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
   }
 }
 
+// ------------------------------------------------------------------------- resident-weight kernels
+// Persistent variants for the hot edge MLP (bf16, every layer H -> H, <= 4 Linears): all packed
+// weights of the chain live in LDS for the whole launch (4 x 32 KB at H = 128), so the 8 waves of
+// a block never synchronise after the prologue and each wave streams its own 32-row tiles —
+// one wave's gathers overlap the other waves' MFMA chains. One block per CU.
+constexpr int RES_WPB = 8;
+constexpr int RES_BLOCK = 64 * RES_WPB;
+constexpr int RES_MAXL = 4;
+
+template <typename T, int NT>
+constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
+
+template <typename T, int NT>
+__global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
+  constexpr int H = 32 * NT;
+  constexpr int NR = 16 * NT;
+  constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;
+  constexpr int LAYER = res_layer_units<T, NT>();
+  __shared__ uint4 wres[RES_MAXL * LAYER];
+  for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int ntiles = (a.rows + 31) / 32;
+  const agn_seg& sg = a.seg[0];
+  for (int tile = blockIdx.x * RES_WPB + (threadIdx.x >> 6); tile < ntiles; tile += gridDim.x * RES_WPB) {
+    cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    const int rr = valid ? row : a.rows - 1;
+    f32x16 acc[NT];
+    BOp<T, NR> b;
+    if (a.proj) {
+      const T* P = reinterpret_cast<const T*>(a.proj);
+      const T* ps = P + (size_t)a.src[rr] * (2 * H);
+      const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int f0 = 32 * t + 8 * q + 4 * h;
+          const f32x4 x = load4(ps + f0), y = load4(pd + f0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = x[e] + y[e];
+        }
+    } else {
+      acc_bias<NT, true>(acc, a.bias[0], H, h);
+    }
+    {
+      float v[NR];
+      load_row<T, NR, true>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, H, h);
+      b.set(v);
+    }
+    gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
+    for (int l = 1; l < a.nlin; ++l) {
+      cbarrier();
+      b.template set_relu<NT>(acc);
+      if (a.act[l - 1] && valid) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h);
+      acc_bias<NT, true>(acc, a.bias[l], H, h);
+      gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
+    }
+    // epilogue: LayerNorm, residual, store
+    float mean = 0.f, rstd = 1.f;
+    if (a.use_ln) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
+      s += xor32(s);
+      mean = s / (float)H;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const float d = acc[i / 16][i % 16] - mean;
+        q += d * d;
+      }
+      q += xor32(q);
+      rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
+      if (a.stats && valid && h == 0) {
+        a.stats[2 * (size_t)row] = mean;
+        a.stats[2 * (size_t)row + 1] = rstd;
+      }
+    }
+    T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * H : nullptr;
+    const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
+    T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
+#pragma unroll
+    for (int q = 0; q < NR / 4; ++q) {
+      const int f0 = 8 * q + 4 * h;
+      f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
+                 acc[q / 4][4 * (q % 4) + 3]};
+      if (a.use_ln) {
+        if (hp && valid) store4(hp + f0, v);
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
+      }
+      if (rp) {
+        const f32x4 r = load4(rp + f0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = round_t<T>(v[e]) + r[e];
+      }
+      if (valid) store4(op + f0, v);
+    }
+  }
+}
+
+template <typename T, int NT>
+__global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp_bwd_args a) {
+  constexpr int H = 32 * NT;
+  constexpr int NR = 16 * NT;
+  constexpr int NP = (NR >= 32) ? NR / 32 : 1;
+  constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;
+  constexpr int LAYER = res_layer_units<T, NT>();
+  __shared__ uint4 wres[RES_MAXL * LAYER];
+  __shared__ float lnp[RES_WPB][2][H];
+  for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int c = lane & 31, h = lane >> 5;
+  const int wid = threadIdx.x >> 6;
+  const int ntiles = (a.rows + 31) / 32;
+  float pg[NP], pb[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (int tile = blockIdx.x * RES_WPB + wid; tile < ntiles; tile += gridDim.x * RES_WPB) {
+    cbarrier();
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    const int rr = valid ? row : a.rows - 1;
+    float A[NR];
+    load_grad<T, NR, true>(A, a, rr, valid, h);
+    if (a.use_ln) {
+      const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
+      const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * H;
+      float B[NR];
+      float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < NR / 4; ++q) {
+        const int f0 = 8 * q + 4 * h;
+        const f32x4 hv = load4(hp + f0);
+        const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (hv[e] - mean) * rstd;
+          const float gg = A[4 * q + e] * gm[e];
+          c1 += gg;
+          c2 += gg * xh;
+          B[4 * q + e] = A[4 * q + e] * xh;
+        }
+      }
+      c1 += xor32(c1);
+      c2 += xor32(c2);
+      c1 /= (float)H;
+      c2 /= (float)H;
+      if (a.ln_partial) {
+        butterfly_reduce<NR>(B, lane);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) pg[i] += B[i];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) B[i] = A[i];
+        butterfly_reduce<NR>(B, lane);
+#pragma unroll
+        for (int i = 0; i < NP; ++i) pb[i] += B[i];
+      }
+#pragma unroll
+      for (int q = 0; q < NR / 4; ++q) {
+        const int f0 = 8 * q + 4 * h;
+        const f32x4 hv = load4(hp + f0);
+        const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float xh = (hv[e] - mean) * rstd;
+          A[4 * q + e] = (A[4 * q + e] * gm[e] - c1 - xh * c2) * rstd;
+        }
+      }
+    }
+    f32x16 acc[NT];
+    BOp<T, NR> b;
+    for (int l = a.nlin - 1; l >= 0; --l) {
+      cbarrier();
+      if (a.gpre[l] && valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, H, A, h);
+      b.set(A);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+      if (l > 0) {
+        gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
+        float m[NR];
+        load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? acc[i / 16][i % 16] : 0.f;
+      } else if (a.din[0]) {
+        gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
+        float v[NR];
+        acc_to_regs<NT, NR>(v, acc);
+        if (a.din_resid[0]) {
+          float g[NR];
+          load_grad<T, NR, true>(g, a, rr, valid, h);
+#pragma unroll
+          for (int i = 0; i < NR; ++i) v[i] += g[i];
+        }
+        if (valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, H, v, h);
+      }
+    }
+  }
+  if (a.use_ln && a.ln_partial) {
+    const bool canon = (NR >= 32) || ((c % (32 / (NR < 32 ? NR : 32))) == 0);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int f = feat_of((c * NR) / 32 + i, h);
+      if (canon) { lnp[wid][0][f] = pg[i]; lnp[wid][1][f] = pb[i]; }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * H; i += RES_BLOCK) {
+      const int q = i / H, f = i - q * H;
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < RES_WPB; ++w) s += lnp[w][q][f];
+      a.ln_partial[(size_t)blockIdx.x * 2 * H + i] = s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- packing
 // A operand of Y^T = A * X^T: A[r][k] = trans ? W[k][r] : W[r][k]  (W row-major, ld)
 template <typename S>
@@ -486,6 +709,34 @@ inline int launch_status() {
     }                                                                              \
   } while (0)
 
+namespace {
+int g_cus = 0;
+int num_cus() {
+  if (g_cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) g_cus = p.multiProcessorCount;
+    if (g_cus <= 0) g_cus = 256;
+  }
+  return g_cus;
+}
+int res_blocks(int rows) {
+  const int tiles = (rows + 31) / 32;
+  const int need = (tiles + RES_WPB - 1) / RES_WPB;
+  const int cap = num_cus();  // 128 KB of resident weights: one block per CU
+  return need < cap ? (need > 0 ? need : 1) : cap;
+}
+bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
+  return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
+         a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k == 128 && a->out_dim == 128 && a->out_ld == 128 &&
+         a->seg[0].ld % 4 == 0 && a->rows >= 64 * 1024;
+}
+bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
+  return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
+         a->in_dim == 128 && a->din_nseg == 1 && a->din_k[0] == 128 && a->rows >= 64 * 1024;
+}
+}  // namespace
+
 extern "C" {
 
 int agn_version(void) { return 1; }
@@ -530,6 +781,11 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   }
   if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
   if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
+  if (res_fwd_ok(a, vec)) {
+    dim3 g(res_blocks(a->rows));
+    hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
+    return launch_status();
+  }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));
   AGN_DISPATCH(mlp_fwd_kernel);
   return launch_status();
@@ -545,7 +801,15 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
     if (s + 1 < a->din_nseg && (a->din_k[s] % 32) != 0) return AGN_E_SHAPE;
   }
   const bool vec = (a->out_dim == a->hidden);
+  agn_mlp_bwd_args* am = const_cast<agn_mlp_bwd_args*>(a);
+  if (res_bwd_ok(a, vec)) {
+    dim3 g(res_blocks(a->rows));
+    am->ln_rows = (int)g.x;
+    hipLaunchKernelGGL((mlp_bwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
+    return launch_status();
+  }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));
+  am->ln_rows = (int)grid.x;
   AGN_DISPATCH(mlp_bwd_kernel);
   return launch_status();
 }

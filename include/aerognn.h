@@ -88,7 +88,7 @@ typedef struct {
   int out_dim;
   int in_dim;      /* K of layer 0 (sum of segment widths in forward) */
   int use_ln;
-  int _unused;
+  int ln_rows;     /* out: rows of ln_partial written (<= agn_mlp_bwd_nwaves(rows)) */
   const void* wtpk[AGN_MAX_LIN];   /* packed TRANSPOSED weights (agn_pack, trans = 1) */
   const void* act[AGN_MAX_LIN];
   const void* hpre;
@@ -182,8 +182,10 @@ int agn_radix_sort_u64(uint64_t* keys, int32_t* vals, int n, int bits, uint64_t*
 /* CSR row pointer of sorted int keys: ptr[v] = first i with key[i] >= v, v = 0..nrows */
 int agn_row_ptr(const int32_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream);
 
-/* exclusive prefix sum of n int32 (single launch); *total (optional) = sum */
-int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, void* stream);
+/* exclusive prefix sum of n int32; *total (optional) = sum; scratch: agn_scan_temp_bytes(n) */
+size_t agn_scan_temp_bytes(int n);
+int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, int32_t* scratch,
+                           void* stream);
 /* same as agn_row_ptr for sorted int64 keys (PyG `batch` vectors) */
 int agn_row_ptr_i64(const int64_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream);
 

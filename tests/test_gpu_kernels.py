@@ -114,3 +114,14 @@ def test_segment_sum_and_gather(dtype):
     gather_rows(777, k, idx.to(DEV), out, o2, cnt_ptr=ptr.to(DEV), add=add.to(DEV))
     ref2 = out.cpu().double()[idx.long()] / counts.clamp(min=1).double()[idx.long()][:, None] + add.double()
     assert rel_l2(o2.cpu(), ref2) <= tol
+
+
+@pytest.mark.parametrize("n", [1, 5, 4096, 4097, 300001, 2_000_000])
+def test_exclusive_scan(n):
+    from aerognn.graph import exclusive_scan
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = torch.randint(0, 50, (n,), generator=g, dtype=torch.int32)
+    out = exclusive_scan(x.to(DEV)).cpu().long()
+    ref = torch.zeros(n + 1, dtype=torch.long)
+    ref[1:] = torch.cumsum(x.long(), 0)
+    assert torch.equal(out, ref)
