@@ -66,6 +66,81 @@ AGN_DEV void store4_masked(T* row, int f0, int k, bool vec_ok, f32x4 v) {
     if (f0 + q < k) row[f0 + q] = from_f<T>(v[q]);
 }
 
+// ---------------------------------------------------------------- 16-B row I/O (acc layout)
+// A full row of H features in acc layout is split over lanes c and c+32 in 4-feature chunks
+// (group q: features 8q+4h..8q+4h+3). For bf16 that is 8 B per lane per access; exchanging
+// halves with v_permlane32_swap (cdna_hip_programming.md T21) lets each lane move 8
+// contiguous features (16 B) instead: pair i = groups (2i, 2i+1) = features 16i..16i+15,
+// lane half h reads/writes features 16i+8h..16i+8h+7. Every lane must execute these
+// (uniform control flow); `valid` only masks the final store.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+AGN_DEV void swap_halves(uint32_t& a, uint32_t& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+AGN_DEV uint32_t pack2(float x, float y) { return __builtin_bit_cast(uint32_t, bf16x2{(bf16)x, (bf16)y}); }
+AGN_DEV float lo_bf16(uint32_t u) { return __uint_as_float(u << 16); }
+AGN_DEV float hi_bf16(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+
+// o[0..3] = features 16i+4h.., o[4..7] = 16i+8+4h.. (acc registers 8i..8i+7)
+AGN_DEV void load8_w(float (&o)[8], const bf16* rowp, int i, int h) {
+  const u32x4 x = *reinterpret_cast<const u32x4*>(rowp + 16 * i + 8 * h);
+  uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  o[0] = lo_bf16(a0); o[1] = hi_bf16(a0); o[2] = lo_bf16(a1); o[3] = hi_bf16(a1);
+  o[4] = lo_bf16(b0); o[5] = hi_bf16(b0); o[6] = lo_bf16(b1); o[7] = hi_bf16(b1);
+}
+AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
+  const f32x4 x = load4(rowp + 16 * i + 4 * h), y = load4(rowp + 16 * i + 8 + 4 * h);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { o[e] = x[e]; o[4 + e] = y[e]; }
+}
+AGN_DEV void store8_w(bf16* rowp, int i, int h, const float (&v)[8], bool valid) {
+  uint32_t a0 = pack2(v[0], v[1]), a1 = pack2(v[2], v[3]), b0 = pack2(v[4], v[5]), b1 = pack2(v[6], v[7]);
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  if (valid) *reinterpret_cast<u32x4*>(rowp + 16 * i + 8 * h) = u32x4{a0, a1, b0, b1};
+}
+AGN_DEV void store8_w(float* rowp, int i, int h, const float (&v)[8], bool valid) {
+  if (!valid) return;
+  store4(rowp + 16 * i + 4 * h, f32x4{v[0], v[1], v[2], v[3]});
+  store4(rowp + 16 * i + 8 + 4 * h, f32x4{v[4], v[5], v[6], v[7]});
+}
+template <typename T, int NR>
+AGN_DEV void load_row_w(float (&v)[NR], const T* rowp, int h) {
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    float o[8];
+    load8_w(o, rowp, i, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
+  }
+}
+template <typename T, int NR>
+AGN_DEV void add_row_w(float (&v)[NR], const T* rowp, int h) {
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    float o[8];
+    load8_w(o, rowp, i, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[8 * i + e] += o[e];
+  }
+}
+template <typename T, int NR>
+AGN_DEV void store_row_w(T* rowp, const float (&v)[NR], int h, bool valid) {
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = v[8 * i + e];
+    store8_w(rowp, i, h, o, valid);
+  }
+}
+
 // Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
 // rows) above the MFMA chain, where they would sit live in registers across every layer.
 AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
@@ -127,14 +202,15 @@ template <int NR> struct BOp<bf16, NR> {
 #pragma unroll
       for (int j = 0; j < 8; ++j) u[i][j] = (bf16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
   }
-  // store the packed activations as a row of `H` bf16 (two 4-feature chunks per unit)
-  AGN_DEV void store(bf16* rowp, int h) const {
+  // store the packed activations as a row of `H` bf16, 16 B per lane (see store8_w)
+  AGN_DEV void store(bf16* rowp, int h, bool valid) const {
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
-      const bf16x4 lo = {u[i][0], u[i][1], u[i][2], u[i][3]};
-      const bf16x4 hi = {u[i][4], u[i][5], u[i][6], u[i][7]};
-      *reinterpret_cast<bf16x4*>(rowp + 16 * i + 4 * h) = lo;
-      *reinterpret_cast<bf16x4*>(rowp + 16 * i + 8 + 4 * h) = hi;
+      const u32x4 x = __builtin_bit_cast(u32x4, u[i]);
+      uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+      swap_halves(a0, b0);
+      swap_halves(a1, b1);
+      if (valid) *reinterpret_cast<u32x4*>(rowp + 16 * i + 8 * h) = u32x4{a0, a1, b0, b1};
     }
   }
 };
@@ -155,7 +231,8 @@ template <int NR> struct BOp<float, NR> {
 #pragma unroll
     for (int i = 0; i < NR; ++i) u[i] = fmaxf(acc[i / 16][i % 16], 0.f);
   }
-  AGN_DEV void store(float* rowp, int h) const {
+  AGN_DEV void store(float* rowp, int h, bool valid) const {
+    if (!valid) return;
 #pragma unroll
     for (int q = 0; q < NR / 4; ++q)
       *reinterpret_cast<f32x4*>(rowp + 8 * q + 4 * h) = f32x4{u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3]};

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       __syncthreads();
       stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
       b.template set_relu<NT>(acc);
-      if (a.act[l - 1] && valid) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h);
+      if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       acc_bias<NT, VEC>(acc, a.bias[l], outl, h);
       __syncthreads();
       if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
@@ -441,31 +441,30 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       const T* ps = P + (size_t)a.src[rr] * (2 * H);
       const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
+      for (int i = 0; i < NR / 8; ++i) {
+        float x[8], y[8];
+        load8_w(x, ps, i, h);
+        load8_w(y, pd, i, h);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int f0 = 32 * t + 8 * q + 4 * h;
-          const f32x4 x = load4(ps + f0), y = load4(pd + f0);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = x[e] + y[e];
-        }
+        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
+      }
     } else {
       acc_bias<NT, true>(acc, a.bias[0], H, h);
     }
     {
       float v[NR];
-      load_row<T, NR, true>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, H, h);
+      load_row_w<T, NR>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
       b.set(v);
     }
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
-      if (a.act[l - 1] && valid) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h);
+      if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       acc_bias<NT, true>(acc, a.bias[l], H, h);
       gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
     }
-    // epilogue: LayerNorm, residual, store
+    // epilogue: LayerNorm, residual, store (8 features per lane at a time)
     float mean = 0.f, rstd = 1.f;
     if (a.use_ln) {
       float s = 0.f;
@@ -490,25 +489,47 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
 #pragma unroll
-    for (int q = 0; q < NR / 4; ++q) {
-      const int f0 = 8 * q + 4 * h;
-      f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
-                 acc[q / 4][4 * (q % 4) + 3]};
-      if (a.use_ln) {
-        if (hp && valid) store4(hp + f0, v);
-        const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+    for (int i = 0; i < NR / 8; ++i) {
+      float v[8];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
+      for (int e = 0; e < 8; ++e) v[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
+      if (a.use_ln) {
+        if (hp) store8_w(hp, i, h, v, valid);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int f0 = 16 * i + 8 * j + 4 * h;
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[4 * j + e] = (v[4 * j + e] - mean) * rstd * g4[e] + b4[e];
+        }
       }
       if (rp) {
-        const f32x4 r = load4(rp + f0);
+        float r[8];
+        load8_w(r, rp, i, h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = round_t<T>(v[e]) + r[e];
+        for (int e = 0; e < 8; ++e) v[e] = round_t<T>(v[e]) + r[e];
       }
-      if (valid) store4(op + f0, v);
+      store8_w(op, i, h, v, valid);
     }
   }
+}
+
+template <typename T, int NR>
+AGN_DEV void load_grad_w(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
+  load_row_w<T, NR>(g, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, h);
+  if (a.g2) add_row_w<T, NR>(g, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
+  if (!valid) {
+#pragma unroll
+    for (int i = 0; i < NR; ++i) g[i] = 0.f;
+  }
+}
+
+template <typename T, int NR>
+AGN_DEV void add_grad_w(float (&v)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
+  if (!valid) return;  // (lanes c, c+32 share `valid`: the swaps inside stay pairwise-uniform)
+  add_row_w<T, NR>(v, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, h);
+  if (a.g2) add_row_w<T, NR>(v, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
 }
 
 template <typename T, int NT>
@@ -535,24 +556,28 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
     float A[NR];
-    load_grad<T, NR, true>(A, a, rr, valid, h);
+    load_grad_w<T, NR>(A, a, rr, valid, h);
     if (a.use_ln) {
       const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
       const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * H;
       float B[NR];
       float c1 = 0.f, c2 = 0.f;
 #pragma unroll
-      for (int q = 0; q < NR / 4; ++q) {
-        const int f0 = 8 * q + 4 * h;
-        const f32x4 hv = load4(hp + f0);
-        const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+      for (int i = 0; i < NR / 8; ++i) {
+        float hv[8];
+        load8_w(hv, hp, i, h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xh = (hv[e] - mean) * rstd;
-          const float gg = A[4 * q + e] * gm[e];
-          c1 += gg;
-          c2 += gg * xh;
-          B[4 * q + e] = A[4 * q + e] * xh;
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + 16 * i + 8 * j + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * i + 4 * j + e;
+            const float xh = (hv[4 * j + e] - mean) * rstd;
+            const float gg = A[r] * gm[e];
+            c1 += gg;
+            c2 += gg * xh;
+            B[r] = A[r] * xh;
+          }
         }
       }
       c1 += xor32(c1);
@@ -570,14 +595,18 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
         for (int i = 0; i < NP; ++i) pb[i] += B[i];
       }
 #pragma unroll
-      for (int q = 0; q < NR / 4; ++q) {
-        const int f0 = 8 * q + 4 * h;
-        const f32x4 hv = load4(hp + f0);
-        const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+      for (int i = 0; i < NR / 8; ++i) {
+        float hv[8];
+        load8_w(hv, hp, i, h);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float xh = (hv[e] - mean) * rstd;
-          A[4 * q + e] = (A[4 * q + e] * gm[e] - c1 - xh * c2) * rstd;
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + 16 * i + 8 * j + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * i + 4 * j + e;
+            const float xh = (hv[4 * j + e] - mean) * rstd;
+            A[r] = (A[r] * gm[e] - c1 - xh * c2) * rstd;
+          }
         }
       }
     }
@@ -585,27 +614,22 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
     BOp<T, NR> b;
     for (int l = a.nlin - 1; l >= 0; --l) {
       cbarrier();
-      if (a.gpre[l] && valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, H, A, h);
+      if (a.gpre[l]) store_row_w<T, NR>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, A, h, valid);
       b.set(A);
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
       if (l > 0) {
         gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
         float m[NR];
-        load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
+        load_row_w<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, h);
 #pragma unroll
         for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? acc[i / 16][i % 16] : 0.f;
       } else if (a.din[0]) {
         gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
         float v[NR];
         acc_to_regs<NT, NR>(v, acc);
-        if (a.din_resid[0]) {
-          float g[NR];
-          load_grad<T, NR, true>(g, a, rr, valid, h);
-#pragma unroll
-          for (int i = 0; i < NR; ++i) v[i] += g[i];
-        }
-        if (valid) store_row<T, NR, true>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, H, v, h);
+        if (a.din_resid[0]) add_grad_w<T, NR>(v, a, rr, true, h);
+        store_row_w<T, NR>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, v, h, valid);
       }
     }
   }
@@ -729,7 +753,7 @@ int res_blocks(int rows) {
 bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
   return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
          a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k == 128 && a->out_dim == 128 && a->out_ld == 128 &&
-         a->seg[0].ld % 4 == 0 && a->rows >= 64 * 1024;
+         a->seg[0].ld % 8 == 0 && a->rows >= 64 * 1024;
 }
 bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
   return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&

@@ -115,7 +115,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--mode", default="train", choices=["train", "fwd"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    ap.add_argument("--traffic", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                                      "r1_pmc_traffic.json"),
+                    help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels")
     args = ap.parse_args()
 
     from aerognn import core, dist as D
@@ -184,8 +186,8 @@ def main():
         tag, (n, ms, by, fl) = dom
         ach = by / n / (ms / n * 1e-3) / 1e9
         traffic = None
-        if args.traffic and os.path.exists(args.traffic):
-            traffic = json.load(open(args.traffic)).get(tag)
+        if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and args.mode == "train":
+            traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(tag)
         roof = {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "alg_bytes_per_launch": by / n, "avg_launch_us": 1e3 * ms / n,
