@@ -29,29 +29,51 @@ template <typename T> struct DwTile;
 template <> struct DwTile<bf16> { static constexpr int LD = 136; };
 template <> struct DwTile<float> { static constexpr int LD = 132; };
 
-// stage rows [r0, r0+64) x cols [c0, c0+128) of a row-major [rows][ld] matrix into LDS,
-// zero-filling out-of-range rows/cols.
+// One 64-row x 128-col stage of a row-major [rows][ld] matrix, moved global -> registers ->
+// LDS so the next stage's loads are in flight while the current stage is on MFMA. Each thread
+// owns NCH 16-B chunks; rows >= rows / cols >= cols read as zero.
 template <typename T>
-AGN_DEV void stage_tile(T* lds, const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0) {
-  constexpr int LD = DwTile<T>::LD;
-  constexpr int PER16 = 16 / sizeof(T);  // elements per 16-B chunk
-  constexpr int CHUNKS = DW_BLK / PER16; // chunks per row
-  const bool vec = ((ld % PER16) == 0) && ((c0 % PER16) == 0) && (cols - c0 >= DW_BLK);
-  for (int i = threadIdx.x; i < DW_ROWS * CHUNKS; i += DW_THREADS) {
-    const int r = i / CHUNKS, ch = i - r * CHUNKS;
-    const int gr = r0 + r;
-    T* dst = lds + r * LD + ch * PER16;
-    if (gr < rows && vec) {
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(g + (size_t)gr * ld + c0 + ch * PER16);
+struct StageRegs {
+  static constexpr int PER16 = 16 / sizeof(T);                  // elements per 16-B chunk
+  static constexpr int CHUNKS = DW_BLK / PER16;                 // chunks per row
+  static constexpr int NCH = DW_ROWS * CHUNKS / DW_THREADS;     // chunks per thread
+  uint4 v[NCH];
+
+  AGN_DEV void load(const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0) {
+    const bool fast = ((ld % PER16) == 0) && ((c0 % PER16) == 0) && (cols - c0 >= DW_BLK) && (r0 + DW_ROWS <= rows);
+    if (fast) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int i = threadIdx.x + j * DW_THREADS;
+        const int r = i / CHUNKS, ch = i - r * CHUNKS;
+        v[j] = *reinterpret_cast<const uint4*>(g + (size_t)(r0 + r) * ld + c0 + ch * PER16);
+      }
     } else {
 #pragma unroll
-      for (int e = 0; e < PER16; ++e) {
-        const int gc = c0 + ch * PER16 + e;
-        dst[e] = (gr < rows && gc < cols) ? g[(size_t)gr * ld + gc] : from_f<T>(0.f);
+      for (int j = 0; j < NCH; ++j) {
+        const int i = threadIdx.x + j * DW_THREADS;
+        const int r = i / CHUNKS, ch = i - r * CHUNKS;
+        const int gr = r0 + r;
+        T e8[PER16];
+#pragma unroll
+        for (int e = 0; e < PER16; ++e) {
+          const int gc = c0 + ch * PER16 + e;
+          e8[e] = (gr < rows && gc < cols) ? g[(size_t)gr * ld + gc] : from_f<T>(0.f);
+        }
+        v[j] = *reinterpret_cast<const uint4*>(e8);
       }
     }
   }
-}
+  AGN_DEV void store(T* lds) const {
+    constexpr int LD = DwTile<T>::LD;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int i = threadIdx.x + j * DW_THREADS;
+      const int r = i / CHUNKS, ch = i - r * CHUNKS;
+      *reinterpret_cast<uint4*>(lds + r * LD + ch * PER16) = v[j];
+    }
+  }
+};
 
 // 8 consecutive rows (k) of one column: two ds_read_b64_tr_b16 (rows kb..kb+3, kb+4..kb+7)
 AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
@@ -94,11 +116,20 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
   float bsum = 0.f;  // bias colsum partial (threads 0..127 own columns m0 + tid)
+  StageRegs<T> rg, rx;
+  if (rbeg < rend) {
+    rg.load(G, d.ldg, rend, d.m, rbeg, m0);
+    rx.load(X, d.ldx, rend, d.k, rbeg, k0);
+  }
   for (int r0 = rbeg; r0 < rend; r0 += DW_ROWS) {
     __syncthreads();
-    stage_tile<T>(sg, G, d.ldg, rend, d.m, r0, m0);
-    stage_tile<T>(sx, X, d.ldx, rend, d.k, r0, k0);
+    rg.store(sg);
+    rx.store(sx);
     __syncthreads();
+    if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
+      rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0);
+      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0);
+    }
     if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK) {
 #pragma unroll 8
       for (int r = 0; r < DW_ROWS; ++r) bsum += to_f(sg[r * LD + threadIdx.x]);

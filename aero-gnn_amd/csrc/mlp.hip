@@ -37,34 +37,43 @@ AGN_DEV void stage_block(uint4* lds, const void* gw, int ku_total, int ot0, int 
   }
 }
 
-// Row I/O in acc layout. VEC: k == 32*NT features, 16/8-byte aligned rows (no masking).
+// Row I/O in acc layout. VEC: k == 32*NT features, 16-B aligned rows -> 16-B per-lane
+// accesses through lane-half exchanges (common.hpp load8_w/store8_w; all lanes of a row pair
+// must be active together). !VEC: masked 4-feature chunks.
 template <typename T, int NR, bool VEC>
 AGN_DEV void load_row(float (&v)[NR], const T* rowp, int k, int h) {
+  if constexpr (VEC) {
+    load_row_w<T, NR>(v, rowp, h);
+  } else {
 #pragma unroll
-  for (int q = 0; q < NR / 4; ++q) {
-    f32x4 x;
-    if (VEC) x = load4(rowp + 8 * q + 4 * h);
-    else x = load4_masked(rowp, 8 * q + 4 * h, k, false);
-    v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+    for (int q = 0; q < NR / 4; ++q) {
+      const f32x4 x = load4_masked(rowp, 8 * q + 4 * h, k, false);
+      v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+    }
   }
 }
 template <typename T, int NR, bool VEC>
 AGN_DEV void add_row(float (&v)[NR], const T* rowp, int k, int h) {
+  if constexpr (VEC) {
+    add_row_w<T, NR>(v, rowp, h);
+  } else {
 #pragma unroll
-  for (int q = 0; q < NR / 4; ++q) {
-    f32x4 x;
-    if (VEC) x = load4(rowp + 8 * q + 4 * h);
-    else x = load4_masked(rowp, 8 * q + 4 * h, k, false);
-    v[4 * q] += x[0]; v[4 * q + 1] += x[1]; v[4 * q + 2] += x[2]; v[4 * q + 3] += x[3];
+    for (int q = 0; q < NR / 4; ++q) {
+      const f32x4 x = load4_masked(rowp, 8 * q + 4 * h, k, false);
+      v[4 * q] += x[0]; v[4 * q + 1] += x[1]; v[4 * q + 2] += x[2]; v[4 * q + 3] += x[3];
+    }
   }
 }
 template <typename T, int NR, bool VEC>
-AGN_DEV void store_row(T* rowp, int k, const float (&v)[NR], int h) {
+AGN_DEV void store_row(T* rowp, int k, const float (&v)[NR], int h, bool valid) {
+  if constexpr (VEC) {
+    store_row_w<T, NR>(rowp, v, h, valid);
+  } else if (valid) {
 #pragma unroll
-  for (int q = 0; q < NR / 4; ++q) {
-    const f32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-    if (VEC) store4(rowp + 8 * q + 4 * h, x);
-    else store4_masked(rowp, 8 * q + 4 * h, k, false, x);
+    for (int q = 0; q < NR / 4; ++q) {
+      const f32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+      store4_masked(rowp, 8 * q + 4 * h, k, false, x);
+    }
   }
 }
 
@@ -106,7 +115,7 @@ AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid,
     }
 #pragma unroll
     for (int i = 0; i < NR; ++i) in[i] = round_t<T>(in[i]);
-    if (s.store && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(s.store) + (size_t)rr * s.k, s.k, in, h);
+    if (s.store) store_row<T, NR, VEC>(reinterpret_cast<T*>(s.store) + (size_t)rr * s.k, s.k, in, h, valid);
   }
 }
 
@@ -143,17 +152,15 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       const T* P = reinterpret_cast<const T*>(a.proj);
       const T* ps = P + (size_t)a.src[rr] * (2 * H);
       const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
-      // one 32-feature tile per round: keeps the gathered rows from all being live at once
+      // one 16-feature pair per round: keeps the gathered rows from all being live at once
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      for (int i = 0; i < NR / 8; ++i) {
         cbarrier();
+        float x[8], y[8];
+        load8_w(x, ps, i, h);
+        load8_w(y, pd, i, h);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int f0 = 32 * t + 8 * q + 4 * h;
-          const f32x4 x = load4(ps + f0), y = load4(pd + f0);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[t][4 * q + e] = x[e] + y[e];
-        }
+        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
       }
     } else {
       acc_bias<NT, VEC>(acc, a.bias[0] ? a.bias[0] + gofs : nullptr, nv0, h);
@@ -209,36 +216,52 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * outd : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs;
+    if constexpr (VEC) {
 #pragma unroll
-    for (int q = 0; q < NR / 4; ++q) {
-      const int f0 = 8 * q + 4 * h;
-      f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
-                 acc[q / 4][4 * (q % 4) + 3]};
-      if (a.use_ln) {
-        if (hp && valid) {
-          if (VEC) store4(hp + f0, v);
-          else store4_masked(hp, f0, outd, false, v);
+      for (int i = 0; i < NR / 8; ++i) {
+        float v8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v8[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
+        if (a.use_ln) {
+          if (hp) store8_w(hp, i, h, v8, valid);
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int f0 = 16 * i + 8 * j + 4 * h;
+            const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
+            const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v8[4 * j + e] = (v8[4 * j + e] - mean) * rstd * g4[e] + b4[e];
+          }
         }
-        f32x4 g4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
-        if (VEC) {
-          g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
-          b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
-        } else {
+        if (rp) {
+          float r8[8];
+          load8_w(r8, rp, i, h);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v8[e] = round_t<T>(v8[e]) + r8[e];
+        }
+        store8_w(op, i, h, v8, valid);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NR / 4; ++q) {
+        const int f0 = 8 * q + 4 * h;
+        f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
+                   acc[q / 4][4 * (q % 4) + 3]};
+        if (a.use_ln) {
+          if (hp && valid) store4_masked(hp, f0, outd, false, v);
+          f32x4 g4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
             if (f0 + e < outd) { g4[e] = a.ln_g[f0 + e]; b4[e] = a.ln_b[f0 + e]; }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
         }
+        if (rp) {
+          const f32x4 r = load4_masked(rp, f0, outd, false);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
-      }
-      if (rp) {
-        const f32x4 r = VEC ? load4(rp + f0) : load4_masked(rp, f0, outd, false);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = round_t<T>(v[e]) + r[e];
-      }
-      if (valid) {
-        if (VEC) store4(op + f0, v);
-        else store4_masked(op, f0, outd, false, v);
+          for (int e = 0; e < 4; ++e) v[e] = round_t<T>(v[e]) + r[e];
+        }
+        if (valid) store4_masked(op, f0, outd, false, v);
       }
     }
   }
@@ -346,7 +369,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
   for (int l = a.nlin - 1; l >= 0; --l) {
     const int Ml = (l == a.nlin - 1) ? M : H;
     const int kuM = units_k<T>(Ml);
-    if (a.gpre[l] && valid) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml, Ml, A, h);
+    if (a.gpre[l]) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml, Ml, A, h, valid);
     b.set(A);
     if (l > 0) {
       __syncthreads();
@@ -382,11 +405,9 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
 #pragma unroll
             for (int i = 0; i < NR; ++i) v[i] += g[i];
           }
-          if (valid) {
-            T* dp = reinterpret_cast<T*>(a.din[s]) + (size_t)row * ks;
-            if (VEC && ks == H) store_row<T, NR, true>(dp, ks, v, h);
-            else store_row<T, NR, false>(dp, ks, v, h);
-          }
+          T* dp = reinterpret_cast<T*>(a.din[s]) + (size_t)row * ks;
+          if (VEC && ks == H) store_row<T, NR, true>(dp, ks, v, h, valid);
+          else store_row<T, NR, false>(dp, ks, v, h, valid);
         }
         koff += ks;
       }
@@ -797,11 +818,11 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   if (!a || a->rows < 0 || a->nlin < 1 || a->nlin > AGN_MAX_LIN || a->nseg < 1 || a->nseg > AGN_MAX_SEG)
     return AGN_E_ARG;
   if (a->rows == 0) return 0;
-  bool vec = (a->out_ld % 4 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
+  bool vec = (a->out_ld % 8 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
   for (int s = 0; s < a->nseg; ++s) {
     if (a->seg[s].k < 1 || a->seg[s].k > a->hidden) return AGN_E_SHAPE;
     if (s + 1 < a->nseg && (a->seg[s].k % 32) != 0) return AGN_E_SHAPE;
-    if (a->seg[s].k != a->hidden || a->seg[s].ld % 4 != 0) vec = false;
+    if (a->seg[s].k != a->hidden || a->seg[s].ld % 8 != 0) vec = false;
   }
   if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
   if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
