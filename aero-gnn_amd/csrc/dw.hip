@@ -183,32 +183,56 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum;
 }
 
-// out[m][k] = sum_s partial[s][m][k] (m < M, k < K), fixed order over s; 4 columns per thread
-__global__ void wgrad_reduce_kernel(const agn_wgrad_batch b, int nsplit) {
+// out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns 64 column quads (256
+// floats of the [mpad][kpad] slab); its RED_G thread groups each sum the splits s = g,
+// g + RED_G, ... and the group partials are combined in LDS in group order: a fixed
+// summation order (deterministic), with RED_G x 64 16-B loads in flight per block.
+constexpr int RED_G = 8;
+__global__ __launch_bounds__(64 * RED_G) void wgrad_reduce_kernel(const agn_wgrad_batch b, int nsplit) {
+  __shared__ f32x4 part[RED_G][64];
+  __shared__ float bpart[RED_G][64];
   const agn_wgrad_desc& d = b.d[blockIdx.y];
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK, nMb = (d.m + DW_BLK - 1) / DW_BLK;
   const int kpad = nKb * DW_BLK, mpad = nMb * DW_BLK;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // over m * kpad / 4
   const size_t slab = (size_t)mpad * kpad;
   const int kq = kpad / 4;
-  if (idx < d.m * kq) {
-    const int m = idx / kq, k0 = 4 * (idx - m * kq);
-    if (k0 < d.k) {
-      f32x4 s = {0.f, 0.f, 0.f, 0.f};
-      const float* p = d.dw_partial + (size_t)m * kpad + k0;
-      for (int sp = 0; sp < nsplit; ++sp) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(p + sp * slab);
-        s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (k0 + e < d.k) d.dw[(size_t)m * d.ldw + k0 + e] = s[e];
+  const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int qidx = blockIdx.x * 64 + t;  // column quad over [mpad][kpad / 4]
+  const bool in_slab = qidx < mpad * kq;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (in_slab) {
+    const float* p = d.dw_partial + (size_t)qidx * 4;
+    for (int sp = g; sp < nsplit; sp += RED_G) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(p + sp * slab);
+      s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
     }
   }
-  if (d.db && idx < d.m) {
-    float s = 0.f;
-    for (int sp = 0; sp < nsplit; ++sp) s += d.db_partial[(size_t)sp * mpad + idx];
-    d.db[idx] = s;
+  part[g][t] = s;
+  // bias: block 0.. covers the first 64 bias entries per block
+  const int bi = blockIdx.x * 64 + t;
+  float bs = 0.f;
+  if (d.db && bi < d.m)
+    for (int sp = g; sp < nsplit; sp += RED_G) bs += d.db_partial[(size_t)sp * mpad + bi];
+  bpart[g][t] = bs;
+  __syncthreads();
+  if (g == 0) {
+    f32x4 r = part[0][t];
+    float rb = bpart[0][t];
+#pragma unroll
+    for (int j = 1; j < RED_G; ++j) {
+      const f32x4 v = part[j][t];
+      r[0] += v[0]; r[1] += v[1]; r[2] += v[2]; r[3] += v[3];
+      rb += bpart[j][t];
+    }
+    if (in_slab) {
+      const int m = qidx / kq, k0 = 4 * (qidx - m * kq);
+      if (m < d.m) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k0 + e < d.k) d.dw[(size_t)m * d.ldw + k0 + e] = r[e];
+      }
+    }
+    if (d.db && bi < d.m) d.db[bi] = rb;
   }
 }
 
@@ -222,12 +246,24 @@ __global__ void colsum_stage1(const float* __restrict__ p, int nw, int n, int ch
   part[(size_t)blockIdx.y * n + c] = s;
 }
 
-__global__ void colsum_stage2(const float* __restrict__ part, int nc, int n, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
+// stage 2: RED_G groups per 64 columns, group g sums chunks g, g + RED_G, ..., then the group
+// partials are added in group order (fixed order: deterministic)
+__global__ __launch_bounds__(64 * RED_G) void colsum_stage2(const float* __restrict__ part, int nc, int n,
+                                                           float* __restrict__ out) {
+  __shared__ float red[RED_G][64];
+  const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + t;
   float s = 0.f;
-  for (int r = 0; r < nc; ++r) s += part[(size_t)r * n + c];
-  out[c] = s;
+  if (c < n)
+    for (int r = g; r < nc; r += RED_G) s += part[(size_t)r * n + c];
+  red[g][t] = s;
+  __syncthreads();
+  if (g == 0 && c < n) {
+    float r = red[0][t];
+#pragma unroll
+    for (int j = 1; j < RED_G; ++j) r += red[j][t];
+    out[c] = r;
+  }
 }
 
 inline int launch_status() {
@@ -266,13 +302,13 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
   else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
   else return AGN_E_DTYPE;
-  int maxmk = 1;
+  int maxq = 1;  // column quads of the largest padded slab
   for (int i = 0; i < b->n; ++i) {
-    const int kq = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK / 4;
-    const int v = b->d[i].m * kq > b->d[i].m ? b->d[i].m * kq : b->d[i].m;
-    maxmk = v > maxmk ? v : maxmk;
+    const int kpad = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    const int mpad = ((b->d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxmk + 255) / 256, b->n), dim3(256), 0, st, *b, nsplit);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, b->n), dim3(64 * RED_G), 0, st, *b, nsplit);
   return launch_status();
 }
 
@@ -286,7 +322,7 @@ int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, 
   const int chunk = (nw + scratch_rows - 1) / scratch_rows;
   const int nc = (nw + chunk - 1) / chunk;
   hipLaunchKernelGGL(colsum_stage1, dim3((n + 255) / 256, nc), dim3(256), 0, st, p, nw, n, chunk, scratch);
-  hipLaunchKernelGGL(colsum_stage2, dim3((n + 255) / 256), dim3(256), 0, st, scratch, nc, n, out);
+  hipLaunchKernelGGL(colsum_stage2, dim3((n + 63) / 64), dim3(64 * RED_G), 0, st, scratch, nc, n, out);
   return launch_status();
 }
 

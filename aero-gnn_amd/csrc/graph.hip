@@ -18,29 +18,80 @@ inline int launch_status() {
 }
 
 // ------------------------------------------------------------------ grouped row reductions
+// 8 contiguous elements of a row as floats (16 B of bf16, 2 x 16 B of fp32), masked at k.
+template <typename T>
+AGN_DEV void load8(float (&o)[8], const T* row, int f0, int k, bool vec) {
+  if (vec && f0 + 7 < k) {
+    if constexpr (sizeof(T) == 2) {
+      const u32x4 x = *reinterpret_cast<const u32x4*>(row + f0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { o[2 * i] = lo_bf16(x[i]); o[2 * i + 1] = hi_bf16(x[i]); }
+    } else {
+      const f32x4 x = load4(row + f0), y = load4(row + f0 + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { o[i] = x[i]; o[4 + i] = y[i]; }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (f0 + i < k) ? to_f(row[f0 + i]) : 0.f;
+}
+template <typename T>
+AGN_DEV void store8(T* row, int f0, int k, bool vec, const float (&v)[8]) {
+  if (vec && f0 + 7 < k) {
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<u32x4*>(row + f0) = u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]),
+                                                  pack2(v[6], v[7])};
+    } else {
+      store4(row + f0, f32x4{v[0], v[1], v[2], v[3]});
+      store4(row + f0 + 4, f32x4{v[4], v[5], v[6], v[7]});
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (f0 + i < k) row[f0 + i] = from_f<T>(v[i]);
+}
+
 // out[r] = sum_{j in ptr[r]..ptr[r+1]-1} src[perm ? perm[j] : j]   (/ max(count,1) if mean)
-// 32 threads per row, 4 features per thread per pass; fp32 accumulation in index order.
+// 16 threads per row, 8 features (16 B of bf16) per thread per pass; fp32 accumulation in
+// index order (two rows' loads in flight per step, summed in order).
+constexpr int SEG_TPR = 16;
 template <typename T>
 __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const int32_t* __restrict__ ptr,
                                                           const int32_t* __restrict__ perm, const T* __restrict__ src,
                                                           int src_ld, T* __restrict__ out, int out_ld, int mean) {
-  const int sub = threadIdx.x & 31;
-  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int sub = threadIdx.x & (SEG_TPR - 1);
+  const int r = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
   if (r >= rows) return;
   const int beg = ptr[r], end = ptr[r + 1];
-  const bool vec = ((k & 3) == 0) && ((src_ld & 3) == 0) && ((out_ld & 3) == 0);
-  for (int f0 = 4 * sub; f0 < k; f0 += 128) {
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int j = beg; j < end; ++j) {
-      const int e = perm ? perm[j] : j;
-      const f32x4 x = load4_masked(src + (size_t)e * src_ld, f0, k, vec);
-      s[0] += x[0]; s[1] += x[1]; s[2] += x[2]; s[3] += x[3];
+  constexpr int A = 16 / sizeof(T);
+  const bool vec = ((k % A) == 0) && ((src_ld % A) == 0) && ((out_ld % A) == 0) &&
+                   ((((uintptr_t)src) | ((uintptr_t)out)) & 15) == 0;
+  for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int j = beg;
+    for (; j + 1 < end; j += 2) {
+      const int e0 = perm ? perm[j] : j, e1 = perm ? perm[j + 1] : j + 1;
+      float x[8], y[8];
+      load8(x, src + (size_t)e0 * src_ld, f0, k, vec);
+      load8(y, src + (size_t)e1 * src_ld, f0, k, vec);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
+    }
+    if (j < end) {
+      const int e0 = perm ? perm[j] : j;
+      float x[8];
+      load8(x, src + (size_t)e0 * src_ld, f0, k, vec);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += x[i];
     }
     if (mean) {
       const float cnt = (float)max(end - beg, 1);
-      s[0] /= cnt; s[1] /= cnt; s[2] /= cnt; s[3] /= cnt;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] /= cnt;
     }
-    store4_masked(out + (size_t)r * out_ld, f0, k, vec, s);
+    store8(out + (size_t)r * out_ld, f0, k, vec, s);
   }
 }
 
@@ -51,23 +102,30 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const
                                                           const int32_t* __restrict__ cnt_ptr,
                                                           const T* __restrict__ add, int add_ld,
                                                           T* __restrict__ out, int out_ld) {
-  const int sub = threadIdx.x & 31;
-  const int r = blockIdx.x * 8 + (threadIdx.x >> 5);
+  const int sub = threadIdx.x & (SEG_TPR - 1);
+  const int r = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
   if (r >= rows) return;
   const int s = idx ? idx[r] : r;
-  const bool vec = ((k & 3) == 0) && ((src_ld & 3) == 0) && ((out_ld & 3) == 0) && ((add_ld & 3) == 0);
+  constexpr int A = 16 / sizeof(T);
+  const bool vec = ((k % A) == 0) && ((src_ld % A) == 0) && ((out_ld % A) == 0) && ((add_ld % A) == 0) &&
+                   ((((uintptr_t)src) | ((uintptr_t)out) | ((uintptr_t)add)) & 15) == 0;
   float div = 1.f;
   if (cnt_ptr) div = (float)max(cnt_ptr[s + 1] - cnt_ptr[s], 1);
-  for (int f0 = 4 * sub; f0 < k; f0 += 128) {
-    f32x4 x = load4_masked(src + (size_t)s * src_ld, f0, k, vec);
-    if (cnt_ptr) { x[0] /= div; x[1] /= div; x[2] /= div; x[3] /= div; }
+  for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
+    float x[8];
+    load8(x, src + (size_t)s * src_ld, f0, k, vec);
+    if (cnt_ptr) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] /= div;
+    }
     if (add) {
       // the reference rounds the gathered value to T before the add (bsms_mgn.py:199-200)
-      const f32x4 y = load4_masked(add + (size_t)r * add_ld, f0, k, vec);
+      float y[8];
+      load8(y, add + (size_t)r * add_ld, f0, k, vec);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) x[e] = round_t<T>(x[e]) + y[e];
+      for (int i = 0; i < 8; ++i) x[i] = round_t<T>(x[i]) + y[i];
     }
-    store4_masked(out + (size_t)r * out_ld, f0, k, vec, x);
+    store8(out + (size_t)r * out_ld, f0, k, vec, x);
   }
 }
 
@@ -414,7 +472,7 @@ __global__ void pool_emit_kernel(int nc, const int32_t* __restrict__ cand_ptr, c
 template <typename T>
 int seg_sum_t(int rows, int k, const int32_t* ptr, const int32_t* perm, const void* src, int src_ld, void* out,
               int out_ld, int mean, hipStream_t st) {
-  hipLaunchKernelGGL(segment_sum_kernel<T>, dim3((rows + 7) / 8), dim3(256), 0, st, rows, k, ptr, perm,
+  hipLaunchKernelGGL(segment_sum_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, ptr, perm,
                      (const T*)src, src_ld, (T*)out, out_ld, mean);
   return launch_status();
 }
@@ -422,7 +480,7 @@ int seg_sum_t(int rows, int k, const int32_t* ptr, const int32_t* perm, const vo
 template <typename T>
 int gather_t(int rows, int k, const int32_t* idx, const void* src, int src_ld, const int32_t* cnt_ptr,
              const void* add, int add_ld, void* out, int out_ld, hipStream_t st) {
-  hipLaunchKernelGGL(gather_rows_kernel<T>, dim3((rows + 7) / 8), dim3(256), 0, st, rows, k, idx, (const T*)src,
+  hipLaunchKernelGGL(gather_rows_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, idx, (const T*)src,
                      src_ld, cnt_ptr, (const T*)add, add_ld, (T*)out, out_ld);
   return launch_status();
 }

@@ -771,6 +771,19 @@ int res_blocks(int rows) {
   const int cap = num_cus();  // 128 KB of resident weights: one block per CU
   return need < cap ? (need > 0 ? need : 1) : cap;
 }
+inline bool al16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+bool fwd_ptrs_aligned(const agn_mlp_fwd_args* a) {
+  bool ok = al16(a->out) && al16(a->resid) && al16(a->proj) && al16(a->hpre);
+  for (int s = 0; s < a->nseg; ++s) ok = ok && al16(a->seg[s].ptr) && al16(a->seg[s].store);
+  for (int l = 0; l < a->nlin; ++l) ok = ok && al16(a->act[l]);
+  return ok;
+}
+bool bwd_ptrs_aligned(const agn_mlp_bwd_args* a) {
+  bool ok = al16(a->g) && al16(a->g2) && al16(a->hpre);
+  for (int s = 0; s < a->din_nseg; ++s) ok = ok && al16(a->din[s]);
+  for (int l = 0; l < a->nlin; ++l) ok = ok && al16(a->act[l]) && al16(a->gpre[l]);
+  return ok;
+}
 bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
   return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
          a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k == 128 && a->out_dim == 128 && a->out_ld == 128 &&
@@ -826,6 +839,9 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   }
   if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
   if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
+  for (int l = 0; l < a->nlin; ++l)
+    if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
+  vec = vec && fwd_ptrs_aligned(a);
   if (res_fwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
     hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
@@ -845,7 +861,9 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
     if (a->din_k[s] > a->hidden) return AGN_E_SHAPE;
     if (s + 1 < a->din_nseg && (a->din_k[s] % 32) != 0) return AGN_E_SHAPE;
   }
-  const bool vec = (a->out_dim == a->hidden);
+  for (int l = 0; l < a->nlin; ++l)
+    if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
+  const bool vec = (a->out_dim == a->hidden) && bwd_ptrs_aligned(a);
   agn_mlp_bwd_args* am = const_cast<agn_mlp_bwd_args*>(a);
   if (res_bwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));

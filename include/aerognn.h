@@ -75,7 +75,7 @@ typedef struct {
   const void* resid;               /* y = resid + mlp(...) (row-major, ld = out_ld) or NULL */
   void* out;
   /* training saves (NULL when not needed) */
-  void* act[AGN_MAX_LIN];          /* relu output of layer l (l < nlin-1), [rows][hidden] */
+  void* act[AGN_MAX_LIN];          /* relu output of layer l (l < nlin-1), [rows][hidden], 16-B aligned */
   void* hpre;                      /* last Linear output before LN, [rows][out_dim] */
   float* stats;                    /* [rows][2] = mean, rstd */
 } agn_mlp_fwd_args;
