@@ -16,14 +16,32 @@ import torch.distributed as dist
 
 
 def init_from_env(backend=None):
-    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*)."""
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*).
+
+    Backend: `backend`, else $AEROGNN_DIST_BACKEND, else "nccl" (= RCCL on ROCm) when a GPU is
+    present and "gloo" otherwise. gloo with device tensors stages through host memory
+    (rehearsing N ranks on one GPU; never the production path)."""
     if not dist.is_available() or int(os.environ.get("WORLD_SIZE", "1")) <= 1:
         return 0, 1
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = os.environ.get("AEROGNN_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         dist.init_process_group(backend=backend)
     return dist.get_rank(), dist.get_world_size()
+
+
+def _host_staged() -> bool:
+    return dist.get_backend() == "gloo"
+
+
+def all_reduce_(t, async_op=False):
+    """SUM all-reduce in place; device tensors go through host memory under gloo."""
+    if t.is_cuda and _host_staged():
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+        return None
+    return dist.all_reduce(t, async_op=async_op)
 
 
 def world():
@@ -35,20 +53,23 @@ def world():
 def global_count(n_local: int, device) -> float:
     t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
     if world()[1] > 1:
-        dist.all_reduce(t)
+        all_reduce_(t)
     return float(t.item())
 
 
 def mse_sum_loss(pred, y, n_global: float):
-    """sum of squared errors / global element count (== MSELoss on the union batch)."""
-    return ((pred.float() - y.float()) ** 2).sum() / n_global
+    """sum of squared errors / global element count (== MSELoss on the union batch), computed
+    in at least fp32 (bf16 predictions are promoted; fp64 stays fp64)."""
+    dt = torch.promote_types(pred.dtype, torch.float32)
+    return ((pred.to(dt) - y.to(dt)) ** 2).sum() / n_global
 
 
 class GradAllReduce:
     """Flat-bucket gradient all-reduce (SUM) of a module's parameters.
 
-    Gradients are packed into a few contiguous fp32 buckets (~4 for the 2.9M-parameter model,
-    each a single RCCL ring all-reduce, link-bound on xGMI) and unpacked in place.
+    Gradients are packed into a few contiguous buckets in the parameters' own dtype (fp32 master
+    weights: ~4 buckets for the 2.9M-parameter model, each a single RCCL ring all-reduce,
+    link-bound on xGMI) and unpacked in place. A bucket never mixes dtypes.
     """
 
     def __init__(self, params, bucket_bytes=4 << 20):
@@ -56,8 +77,11 @@ class GradAllReduce:
         self.buckets = []
         cur, size = [], 0
         for p in self.params:
+            if cur and cur[-1].dtype != p.dtype:
+                self.buckets.append(cur)
+                cur, size = [], 0
             cur.append(p)
-            size += p.numel() * 4
+            size += p.numel() * p.element_size()
             if size >= bucket_bytes:
                 self.buckets.append(cur)
                 cur, size = [], 0
@@ -71,7 +95,7 @@ class GradAllReduce:
             return
         if self._flat is None:
             dev = self.params[0].device
-            self._flat = [torch.empty(sum(p.numel() for p in b), dtype=torch.float32, device=dev)
+            self._flat = [torch.empty(sum(p.numel() for p in b), dtype=b[0].dtype, device=dev)
                           for b in self.buckets]
         works = []
         for b, flat in zip(self.buckets, self._flat):
@@ -81,9 +105,10 @@ class GradAllReduce:
                 g = p.grad if p.grad is not None else torch.zeros_like(p)
                 flat[o:o + n].copy_(g.reshape(-1))
                 o += n
-            works.append(dist.all_reduce(flat, async_op=True))
+            works.append(all_reduce_(flat, async_op=True))
         for w, b, flat in zip(works, self.buckets, self._flat):
-            w.wait()
+            if w is not None:
+                w.wait()
             o = 0
             for p in b:
                 n = p.numel()

@@ -123,6 +123,7 @@ def main():
     from aerognn import core, dist as D
     rank, ws = D.init_from_env()
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local %= max(1, torch.cuda.device_count())  # ranks > GPUs only when rehearsing on one card
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     nu, nv, S, dtype = CONFIGS[args.config]
@@ -163,6 +164,8 @@ def main():
     prof, core.PROF = core.PROF, None
     if ws > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        if D._host_staged():
+            e = e.cpu()
         torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(e.item())
 

@@ -1,0 +1,102 @@
+"""N>1 data-parallel path on the GPU, rehearsed with 2 ranks sharing the box's one MI355X
+(gloo staged through host memory; on the 8-GPU node the same code runs over RCCL).
+
+1. DP gradients of the HIP model (each rank its own mesh, dist.mse_sum_loss + GradAllReduce)
+   equal the single-process union-batch gradients of the same HIP model (fp32, summation-order
+   tolerance).
+2. `bench.py --gpus 2` under torchrun prints one JSON line with n_gpus == 2.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MESHES = [(24, 16, 0), (20, 12, 1)]
+KW = dict(processor_size=5, num_hidden_layers_node_processor=2, num_hidden_layers_edge_processor=2,
+          num_hidden_layers_node_encoder=2, num_hidden_layers_edge_encoder=2, num_hidden_layers_decoder=2,
+          hidden_dim_processor=128, hidden_dim_node_encoder=128, hidden_dim_edge_encoder=128,
+          hidden_dim_decoder=128, aggregation="add", do_concat_trick=True, num_scales=3,
+          layers_per_scale=1, stride=2)
+
+WORKER = r'''
+import os, sys, json
+sys.path[:0] = [{root!r}, os.path.join({root!r}, "aero-gnn_amd")]
+import numpy as np, torch
+os.environ["AEROGNN_MEMLOG"] = "0"
+from aerognn import dist as D
+from aerognn.meshgen import ellipsoid
+from models.bsms_mgn import BiStridedMeshGraphNet
+rank, ws = D.init_from_env(backend="gloo")
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+model = BiStridedMeshGraphNet(6, 4, 4, **{kw!r}).to(dev)
+nu, nv, seed = {meshes!r}[rank]
+t = {{k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in ellipsoid(nu, nv, seed=seed).items()}}
+n_glob = D.global_count(t["y"].numel(), dev)
+pred = model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"])
+D.mse_sum_loss(pred, t["y"], n_glob).backward()
+D.GradAllReduce(model.parameters())()
+if rank == 0:
+    torch.save({{k: p.grad.cpu() for k, p in model.named_parameters()}}, {out!r})
+torch.distributed.barrier()
+torch.distributed.destroy_process_group()
+'''
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(script_args, timeout):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", AEROGNN_DIST_BACKEND="gloo", AEROGNN_MEMLOG="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}"] + script_args
+    return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+
+
+def test_dp_grads_equal_union_batch_on_gpu(tmp_path):
+    out = str(tmp_path / "g.pt")
+    script = tmp_path / "worker.py"
+    script.write_text(WORKER.format(root=ROOT, kw=KW, meshes=MESHES, out=out))
+    r = _torchrun([str(script)], timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    g_dp = torch.load(out, weights_only=True)
+
+    from aerognn.meshgen import collate, ellipsoid
+    from models.bsms_mgn import BiStridedMeshGraphNet
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = BiStridedMeshGraphNet(6, 4, 4, **KW).to(dev)
+    u = collate([ellipsoid(*m[:2], seed=m[2]) for m in MESHES])
+    u = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in u.items()}
+    pred = model(u["x"], u["edge_attr"], u["edge_index"], batch=u["batch"], pos=u["pos"])
+    torch.nn.functional.mse_loss(pred, u["y"]).backward()
+    errs = []
+    for k, p in model.named_parameters():
+        ref = p.grad.cpu().double()
+        errs.append(float((g_dp[k].double() - ref).norm() / max(float(ref.norm()), 1e-30)))
+    errs = np.array(errs)
+    # fp32 with different (valid) summation orders; ReLU kinks make a few parameters noisier
+    assert np.median(errs) < 1e-5 and errs.max() < 1e-3, (np.median(errs), errs.max())
+
+
+def test_bench_two_ranks_json():
+    r = _torchrun(["bench.py", "--gpus", "2", "--config", "small", "--steps", "2", "--warmup", "1",
+                   "--no-cpu-baseline"], timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
+    assert d["config"]["parallelism"] == "dp2"
