@@ -16,6 +16,7 @@ MAX_LIN = 8
 MAX_SEG = 3
 F32, BF16 = 0, 1
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
+OPT_RESIDENT = 0
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -86,6 +87,7 @@ def lib():
         sig = {
             "agn_version": (i32, []),
             "agn_error_string": (C.c_char_p, [i32]),
+            "agn_set_option": (i32, [i32, i32]),
             "agn_packed_bytes": (C.c_size_t, [i32, i32, i32]),
             "agn_pack": (i32, [vp, i32, i32, vp]),
             "agn_mlp_forward": (i32, [C.POINTER(MlpFwdArgs), vp]),

@@ -202,6 +202,11 @@ template <int NR> struct BOp<bf16, NR> {
 #pragma unroll
       for (int j = 0; j < 8; ++j) u[i][j] = (bf16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
   }
+  // registers 8i..8i+7 (acc order) as floats
+  AGN_DEV void get8(float (&o)[8], int i) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)u[i][j];
+  }
   // store the packed activations as a row of `H` bf16, 16 B per lane (see store8_w)
   AGN_DEV void store(bf16* rowp, int h, bool valid) const {
 #pragma unroll
@@ -230,6 +235,10 @@ template <int NR> struct BOp<float, NR> {
   AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) u[i] = fmaxf(acc[i / 16][i % 16], 0.f);
+  }
+  AGN_DEV void get8(float (&o)[8], int i) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = u[8 * i + j];
   }
   AGN_DEV void store(float* rowp, int h, bool valid) const {
     if (!valid) return;

@@ -96,6 +96,29 @@ AGN_DEV void acc_bias(f32x16 (&acc)[NT], const float* b, int nvalid, int h) {
     for (int r = 0; r < 16; ++r) acc[t][r] = v[16 * t + r];
 }
 
+// bias from an LDS copy of the parameter vector (H floats)
+template <int NT>
+AGN_DEV void acc_bias_lds(f32x16 (&acc)[NT], const float* pv, int h) {
+#pragma unroll
+  for (int q = 0; q < 4 * NT; ++q) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(pv + 8 * q + 4 * h);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+  }
+}
+
+// Stage the per-feature fp32 parameter vectors of a resident chain into LDS:
+// pv[l] = bias of Linear l (0 if absent), pv[RES_MAXL] = LN gamma, pv[RES_MAXL + 1] = LN beta.
+template <int H, int NV>
+AGN_DEV void stage_params(float (*pv)[H], const float* const* bias, int nlin, const float* g, const float* b,
+                          int nthreads) {
+  for (int i = threadIdx.x; i < NV * H; i += nthreads) {
+    const int l = i / H, f = i - l * H;
+    const float* src = l < NV - 2 ? (l < nlin ? bias[l] : nullptr) : (l == NV - 2 ? g : b);
+    pv[l][f] = src ? src[f] : 0.f;
+  }
+}
+
 // Load one input segment for data row `rr` into acc-layout registers.
 template <typename T, int NR, bool VEC>
 AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid, int h) {
@@ -437,6 +460,26 @@ constexpr int RES_MAXL = 4;
 template <typename T, int NT>
 constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
 
+// XCD-aware tile walk: blocks b and b + 8 share an XCD (and its 4 MB L2), so each group of
+// blocks {g, g+8, ...} walks one contiguous eighth of the tiles. Consecutive CSC edge tiles
+// share receivers and nearby senders: their P_s/P_d rows are re-read from the same L2.
+struct ResTiles {
+  int first, end, step;
+  AGN_DEV ResTiles(int ntiles, int wid) {
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+      const int g = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = gridDim.x >> 3;
+      const int per = (ntiles + 7) / 8;
+      first = g * per + bi * RES_WPB + wid;
+      end = min(ntiles, (g + 1) * per);
+      step = nb * RES_WPB;
+    } else {
+      first = blockIdx.x * RES_WPB + wid;
+      end = ntiles;
+      step = gridDim.x * RES_WPB;
+    }
+  }
+};
+
 template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
@@ -444,13 +487,16 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
+  __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
+  stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int c = lane & 31, h = lane >> 5;
   const int ntiles = (a.rows + 31) / 32;
   const agn_seg& sg = a.seg[0];
-  for (int tile = blockIdx.x * RES_WPB + (threadIdx.x >> 6); tile < ntiles; tile += gridDim.x * RES_WPB) {
+  const ResTiles tw(ntiles, threadIdx.x >> 6);
+  for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
@@ -470,19 +516,23 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
       }
     } else {
-      acc_bias<NT, true>(acc, a.bias[0], H, h);
+      acc_bias_lds<NT>(acc, pv[0], h);
     }
     {
       float v[NR];
       load_row_w<T, NR>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
       b.set(v);
     }
+    // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
+    // operand instead of re-reading the row in the epilogue
+    const bool res_in = a.resid == sg.ptr && a.out_ld == sg.ld;
+    const BOp<T, NR> e0 = b;
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
       if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
-      acc_bias<NT, true>(acc, a.bias[l], H, h);
+      acc_bias_lds<NT>(acc, pv[l], h);
       gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
     }
     // epilogue: LayerNorm, residual, store (8 features per lane at a time)
@@ -519,15 +569,16 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int f0 = 16 * i + 8 * j + 4 * h;
-          const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
-          const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(&pv[RES_MAXL][f0]);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(&pv[RES_MAXL + 1][f0]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[4 * j + e] = (v[4 * j + e] - mean) * rstd * g4[e] + b4[e];
         }
       }
       if (rp) {
         float r[8];
-        load8_w(r, rp, i, h);
+        if (res_in) e0.get8(r, i);
+        else load8_w(r, rp, i, h);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = round_t<T>(v[e]) + r[e];
       }
@@ -547,10 +598,22 @@ AGN_DEV void load_grad_w(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool
 }
 
 template <typename T, int NR>
-AGN_DEV void add_grad_w(float (&v)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
-  if (!valid) return;  // (lanes c, c+32 share `valid`: the swaps inside stay pairwise-uniform)
-  add_row_w<T, NR>(v, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, h);
-  if (a.g2) add_row_w<T, NR>(v, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
+AGN_DEV void add_grad_w(float (&v)[NR], const agn_mlp_bwd_args& a, int rr, int h) {
+  // v += (g + g2): the incoming gradient is summed first, as autograd accumulates it
+  const T* g = reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim;
+  if (!a.g2) {
+    add_row_w<T, NR>(v, g, h);
+    return;
+  }
+  const T* g2 = reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim;
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) {
+    float x[8], y[8];
+    load8_w(x, g, i, h);
+    load8_w(y, g2, i, h);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[8 * i + e] += x[e] + y[e];
+  }
 }
 
 template <typename T, int NT>
@@ -562,7 +625,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ float lnp[RES_WPB][2][H];
+  __shared__ __attribute__((aligned(16))) float pg_lds[H];  // LN gamma
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
+  for (int i = threadIdx.x; i < H; i += RES_BLOCK) pg_lds[i] = a.use_ln ? a.ln_g[i] : 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int c = lane & 31, h = lane >> 5;
@@ -571,7 +636,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
   float pg[NP], pb[NP];
 #pragma unroll
   for (int i = 0; i < NP; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
-  for (int tile = blockIdx.x * RES_WPB + wid; tile < ntiles; tile += gridDim.x * RES_WPB) {
+  const ResTiles tw(ntiles, wid);
+  for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
@@ -589,7 +655,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
         load8_w(hv, hp, i, h);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + 16 * i + 8 * j + 4 * h);
+          const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 8 * i + 4 * j + e;
@@ -621,7 +687,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
         load8_w(hv, hp, i, h);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const f32x4 gm = *reinterpret_cast<const f32x4*>(a.ln_g + 16 * i + 8 * j + 4 * h);
+          const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int r = 8 * i + 4 * j + e;
@@ -649,7 +715,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
         gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
         float v[NR];
         acc_to_regs<NT, NR>(v, acc);
-        if (a.din_resid[0]) add_grad_w<T, NR>(v, a, rr, true, h);
+        if (a.din_resid[0]) add_grad_w<T, NR>(v, a, rr, h);
         store_row_w<T, NR>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, v, h, valid);
       }
     }
@@ -784,13 +850,14 @@ bool bwd_ptrs_aligned(const agn_mlp_bwd_args* a) {
   for (int l = 0; l < a->nlin; ++l) ok = ok && al16(a->act[l]) && al16(a->gpre[l]);
   return ok;
 }
+int g_opt_resident = 1;
 bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
-  return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
+  return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
          a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k == 128 && a->out_dim == 128 && a->out_ld == 128 &&
          a->seg[0].ld % 8 == 0 && a->rows >= 64 * 1024;
 }
 bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
-  return vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
+  return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
          a->in_dim == 128 && a->din_nseg == 1 && a->din_k[0] == 128 && a->rows >= 64 * 1024;
 }
 }  // namespace
@@ -798,6 +865,15 @@ bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
 extern "C" {
 
 int agn_version(void) { return 1; }
+
+int agn_set_option(int key, int value) {
+  if (key == AGN_OPT_RESIDENT) {
+    const int old = g_opt_resident;
+    g_opt_resident = value ? 1 : 0;
+    return old;
+  }
+  return AGN_E_ARG;
+}
 
 const char* agn_error_string(int code) {
   switch (code) {

@@ -154,6 +154,11 @@ int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, 
 
 int agn_version(void);
 const char* agn_error_string(int code);
+/* Process-wide kernel-selection options (testing / A-B measurement). Returns the previous value
+ * or AGN_E_ARG. AGN_OPT_RESIDENT: 1 (default) = persistent resident-weight kernels for the
+ * large bf16 H=128 edge MLPs, 0 = always the general kernels (bitwise-identical outputs). */
+enum { AGN_OPT_RESIDENT = 0 };
+int agn_set_option(int key, int value);
 /* bytes of a packed A operand with `m` rows and `k` reduction columns */
 size_t agn_packed_bytes(int m, int k, int dtype);
 /* max_threads >= max over descs of packed 16-B units (or vector length) */
