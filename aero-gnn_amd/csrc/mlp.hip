@@ -143,11 +143,32 @@ AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid,
 }
 
 // ------------------------------------------------------------------------- forward
-template <typename T, int NT, bool VEC>
+// I/O modes of the general kernels (compile-time, chosen on the host per call):
+//   M_VEC : every input segment and the output are H wide (16-B row I/O everywhere)
+//   M_NIN : one PLAIN input of k <= 16 features (encoders: d_n = 6, d_e = 4), output H wide
+//   M_NOUT: H-wide inputs, nlin > 1, output of <= 32 features, no LayerNorm (decoder: d_out = 4)
+//   M_GEN : anything else (masked 4-feature chunks)
+enum { M_VEC = 0, M_GEN = 1, M_NIN = 2, M_NOUT = 3 };
+
+// k <= 16 features of one row into acc-layout registers (features >= k and >= 16 are zero)
+template <typename T, int NR>
+AGN_DEV void load_row_narrow(float (&v)[NR], const T* rowp, int k, int h) {
+#pragma unroll
+  for (int i = 0; i < NR; ++i) v[i] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const f32x4 x = load4_masked(rowp, 8 * q + 4 * h, k, false);
+    v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+  }
+}
+
+template <typename T, int NT, int MODE>
 __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;  // K units of an H-wide input
+  constexpr bool IN_FULL = (MODE == M_VEC || MODE == M_NOUT);
+  constexpr bool OUT_FULL = (MODE == M_VEC || MODE == M_NIN);
   __shared__ uint4 wl[lds_units<T, NT>()];
   const int lane = threadIdx.x & 63;
   const int c = lane & 31, h = lane >> 5;
@@ -186,7 +207,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
       }
     } else {
-      acc_bias<NT, VEC>(acc, a.bias[0] ? a.bias[0] + gofs : nullptr, nv0, h);
+      acc_bias<NT, OUT_FULL || MODE == M_NOUT>(acc, a.bias[0] ? a.bias[0] + gofs : nullptr, nv0, h);
     }
     // ---- layer 0: sum over input segments
     int unit = 0;
@@ -194,40 +215,47 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       const int nu = units_k<T>(a.seg[s].k);
       __syncthreads();
       stage_block(wl, a.wpk[0], ku0, grp * NT, otn0, unit, nu);
-      load_segment<T, NR, VEC>(v, a.seg[s], rr, valid, h);
+      if constexpr (MODE == M_NIN) {
+        load_row_narrow<T, NR>(v, reinterpret_cast<const T*>(a.seg[s].ptr) + (size_t)rr * a.seg[s].ld, a.seg[s].k, h);
+      } else {
+        load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
+      }
       b.set(v);
       __syncthreads();
-      if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
+      if constexpr (IN_FULL) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
+      else if constexpr (MODE == M_NIN) gemm<T, NT, NR, true>(acc, b, nu, wl, nu, NT, lane);
       else gemm<T, NT, NR>(acc, b, nu, wl, nu, otn0, lane);
       unit += nu;
     }
     // ---- hidden layers: relu(acc) -> packed operand -> next Linear (registers only)
     for (int l = 1; l < a.nlin; ++l) {
-      const int outl = (l == a.nlin - 1) ? a.out_dim : H;
+      const bool last = (l == a.nlin - 1);
+      const int outl = last ? a.out_dim : H;
       const int otn = (outl + 31) / 32;
       __syncthreads();
       stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
       b.template set_relu<NT>(acc);
       if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
-      acc_bias<NT, VEC>(acc, a.bias[l], outl, h);
+      if (OUT_FULL || !last) acc_bias<NT, true>(acc, a.bias[l], H, h);
+      else acc_bias<NT, false>(acc, a.bias[l], outl, h);
       __syncthreads();
-      if (VEC) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
+      if (OUT_FULL || !last) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
       else gemm<T, NT, NR>(acc, b, NUH, wl, NUH, otn, lane);
     }
-    // ---- epilogue: LayerNorm, residual, store (in place on the accumulators, 4 features at a time)
+    // ---- epilogue: LayerNorm, residual, store
     const int outd = (a.nlin == 1) ? nv0 : a.out_dim;
     float mean = 0.f, rstd = 1.f;
-    if (a.use_ln) {
+    if (MODE != M_NOUT && a.use_ln) {
       float s = 0.f;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) s += (VEC || feat_of(i, h) < outd) ? acc[i / 16][i % 16] : 0.f;
+      for (int i = 0; i < NR; ++i) s += (OUT_FULL || feat_of(i, h) < outd) ? acc[i / 16][i % 16] : 0.f;
       s += xor32(s);
       mean = s / (float)outd;
       float q = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
         const float d = acc[i / 16][i % 16] - mean;
-        q += (VEC || feat_of(i, h) < outd) ? d * d : 0.f;
+        q += (OUT_FULL || feat_of(i, h) < outd) ? d * d : 0.f;
       }
       q += xor32(q);
       rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
@@ -239,7 +267,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * outd : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs;
-    if constexpr (VEC) {
+    if constexpr (OUT_FULL) {
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float v8[8];
@@ -265,12 +293,14 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         store8_w(op, i, h, v8, valid);
       }
     } else {
+      // M_NOUT: only the first 32 features (acc tile 0) exist; M_GEN: all, masked
+      constexpr int NQ = (MODE == M_NOUT) ? 4 : NR / 4;
 #pragma unroll
-      for (int q = 0; q < NR / 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const int f0 = 8 * q + 4 * h;
         f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
                    acc[q / 4][4 * (q % 4) + 3]};
-        if (a.use_ln) {
+        if (MODE != M_NOUT && a.use_ln) {
           if (hp && valid) store4_masked(hp, f0, outd, false, v);
           f32x4 g4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -291,20 +321,35 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
 }
 
 // ------------------------------------------------------------------------- backward
-template <typename T, int NR, bool VEC>
+template <typename T, int NR, int MODE>
 AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
-  load_row<T, NR, VEC>(g, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, a.out_dim, h);
-  if (a.g2)
-    add_row<T, NR, VEC>(g, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim,
-                        a.out_dim, h);
+  const T* g1 = reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim;
+  const T* g2 = a.g2 ? reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim : nullptr;
+  if constexpr (MODE == M_NOUT) {  // out_dim <= 32: acc tile 0 only
+#pragma unroll
+    for (int i = 0; i < NR; ++i) g[i] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 x = load4_masked(g1, 8 * q + 4 * h, a.out_dim, false);
+      if (g2) {
+        const f32x4 y = load4_masked(g2, 8 * q + 4 * h, a.out_dim, false);
+        x[0] += y[0]; x[1] += y[1]; x[2] += y[2]; x[3] += y[3];
+      }
+      g[4 * q] = x[0]; g[4 * q + 1] = x[1]; g[4 * q + 2] = x[2]; g[4 * q + 3] = x[3];
+    }
+  } else {
+    load_row<T, NR, MODE == M_VEC>(g, g1, a.out_dim, h);
+    if (g2) add_row<T, NR, MODE == M_VEC>(g, g2, a.out_dim, h);
+  }
   if (!valid) {
 #pragma unroll
     for (int i = 0; i < NR; ++i) g[i] = 0.f;
   }
 }
 
-template <typename T, int NT, bool VEC>
+template <typename T, int NT, int MODE>
 __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_args a) {
+  constexpr bool VEC = (MODE == M_VEC);
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NP = (NR >= 32) ? NR / 32 : 1;
@@ -320,8 +365,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
   const int M = a.out_dim;
 
   float A[NR];  // current dL/d(pre-activation)
-  load_grad<T, NR, VEC>(A, a, rr, valid, h);
-  if (a.use_ln) {
+  load_grad<T, NR, MODE>(A, a, rr, valid, h);
+  if (MODE != M_NOUT && a.use_ln) {
     // LayerNorm backward, streamed 4 features at a time (hpre, gamma re-read per chunk)
     const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
     const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * M;
@@ -392,7 +437,11 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
   for (int l = a.nlin - 1; l >= 0; --l) {
     const int Ml = (l == a.nlin - 1) ? M : H;
     const int kuM = units_k<T>(Ml);
-    if (a.gpre[l]) store_row<T, NR, VEC>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml, Ml, A, h, valid);
+    if (a.gpre[l]) {
+      T* gp = reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml;
+      if (VEC || (MODE == M_NOUT && l < a.nlin - 1)) store_row<T, NR, true>(gp, Ml, A, h, valid);
+      else store_row<T, NR, false>(gp, Ml, A, h, valid);
+    }
     b.set(A);
     if (l > 0) {
       __syncthreads();
@@ -424,12 +473,12 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
           if (a.din_resid[s]) {
             cbarrier();
             float g[NR];
-            load_grad<T, NR, VEC>(g, a, rr, valid, h);
+            load_grad<T, NR, MODE>(g, a, rr, valid, h);
 #pragma unroll
             for (int i = 0; i < NR; ++i) v[i] += g[i];
           }
           T* dp = reinterpret_cast<T*>(a.din[s]) + (size_t)row * ks;
-          if (VEC && ks == H) store_row<T, NR, true>(dp, ks, v, h, valid);
+          if (MODE != M_GEN && ks == H) store_row<T, NR, true>(dp, ks, v, h, valid);
           else store_row<T, NR, false>(dp, ks, v, h, valid);
         }
         koff += ks;
@@ -800,24 +849,38 @@ inline int launch_status() {
 
 }  // namespace
 
-#define AGN_LAUNCH(KERNEL, T, NT, VEC) \
-  hipLaunchKernelGGL((KERNEL<T, NT, VEC>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a)
+#define AGN_LAUNCH(KERNEL, T, NT, MODE) \
+  hipLaunchKernelGGL((KERNEL<T, NT, MODE>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a)
 
-#define AGN_DISPATCH(KERNEL)                                                       \
-  do {                                                                             \
-    if (a->dtype == AGN_F32) {                                                     \
-      if (a->hidden == 128) { if (vec) AGN_LAUNCH(KERNEL, float, 4, true); else AGN_LAUNCH(KERNEL, float, 4, false); } \
-      else if (a->hidden == 64) { if (vec) AGN_LAUNCH(KERNEL, float, 2, true); else AGN_LAUNCH(KERNEL, float, 2, false); } \
-      else if (a->hidden == 32) { if (vec) AGN_LAUNCH(KERNEL, float, 1, true); else AGN_LAUNCH(KERNEL, float, 1, false); } \
-      else return AGN_E_HIDDEN;                                                    \
-    } else if (a->dtype == AGN_BF16) {                                             \
-      if (a->hidden == 128) { if (vec) AGN_LAUNCH(KERNEL, bf16, 4, true); else AGN_LAUNCH(KERNEL, bf16, 4, false); } \
-      else if (a->hidden == 64) { if (vec) AGN_LAUNCH(KERNEL, bf16, 2, true); else AGN_LAUNCH(KERNEL, bf16, 2, false); } \
-      else if (a->hidden == 32) { if (vec) AGN_LAUNCH(KERNEL, bf16, 1, true); else AGN_LAUNCH(KERNEL, bf16, 1, false); } \
-      else return AGN_E_HIDDEN;                                                    \
-    } else {                                                                       \
-      return AGN_E_DTYPE;                                                          \
-    }                                                                              \
+#define AGN_FWD_MODES(T, NT)                                   \
+  switch (mode) {                                              \
+    case M_VEC: AGN_LAUNCH(mlp_fwd_kernel, T, NT, M_VEC); break;   \
+    case M_NIN: AGN_LAUNCH(mlp_fwd_kernel, T, NT, M_NIN); break;   \
+    case M_NOUT: AGN_LAUNCH(mlp_fwd_kernel, T, NT, M_NOUT); break; \
+    default: AGN_LAUNCH(mlp_fwd_kernel, T, NT, M_GEN); break;      \
+  }
+#define AGN_BWD_MODES(T, NT)                                   \
+  switch (mode) {                                              \
+    case M_VEC: AGN_LAUNCH(mlp_bwd_kernel, T, NT, M_VEC); break;   \
+    case M_NOUT: AGN_LAUNCH(mlp_bwd_kernel, T, NT, M_NOUT); break; \
+    default: AGN_LAUNCH(mlp_bwd_kernel, T, NT, M_GEN); break;      \
+  }
+
+#define AGN_DISPATCH(MODES)                                                   \
+  do {                                                                        \
+    if (a->dtype == AGN_F32) {                                                \
+      if (a->hidden == 128) { MODES(float, 4) }                               \
+      else if (a->hidden == 64) { MODES(float, 2) }                           \
+      else if (a->hidden == 32) { MODES(float, 1) }                           \
+      else return AGN_E_HIDDEN;                                               \
+    } else if (a->dtype == AGN_BF16) {                                        \
+      if (a->hidden == 128) { MODES(bf16, 4) }                                \
+      else if (a->hidden == 64) { MODES(bf16, 2) }                            \
+      else if (a->hidden == 32) { MODES(bf16, 1) }                            \
+      else return AGN_E_HIDDEN;                                               \
+    } else {                                                                  \
+      return AGN_E_DTYPE;                                                     \
+    }                                                                         \
   } while (0)
 
 namespace {
@@ -907,24 +970,32 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   if (!a || a->rows < 0 || a->nlin < 1 || a->nlin > AGN_MAX_LIN || a->nseg < 1 || a->nseg > AGN_MAX_SEG)
     return AGN_E_ARG;
   if (a->rows == 0) return 0;
-  bool vec = (a->out_ld % 8 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
+  const bool out_full =
+      (a->out_ld % 8 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
+  bool in_full = true;
   for (int s = 0; s < a->nseg; ++s) {
     if (a->seg[s].k < 1 || a->seg[s].k > a->hidden) return AGN_E_SHAPE;
     if (s + 1 < a->nseg && (a->seg[s].k % 32) != 0) return AGN_E_SHAPE;
-    if (a->seg[s].k != a->hidden || a->seg[s].ld % 8 != 0) vec = false;
+    if (a->seg[s].k != a->hidden || a->seg[s].ld % 8 != 0) in_full = false;
   }
   if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
   if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
   for (int l = 0; l < a->nlin; ++l)
     if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
-  vec = vec && fwd_ptrs_aligned(a);
+  int mode = M_GEN;
+  if (fwd_ptrs_aligned(a)) {
+    if (in_full && out_full) mode = M_VEC;
+    else if (out_full && a->nseg == 1 && a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k <= 16) mode = M_NIN;
+    else if (in_full && a->nlin > 1 && a->out_dim <= 32 && !a->use_ln) mode = M_NOUT;
+  }
+  const bool vec = mode == M_VEC;
   if (res_fwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
     hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
     return launch_status();
   }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));
-  AGN_DISPATCH(mlp_fwd_kernel);
+  AGN_DISPATCH(AGN_FWD_MODES);
   return launch_status();
 }
 
@@ -939,7 +1010,12 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
   }
   for (int l = 0; l < a->nlin; ++l)
     if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
-  const bool vec = (a->out_dim == a->hidden) && bwd_ptrs_aligned(a);
+  int mode = M_GEN;
+  if (bwd_ptrs_aligned(a)) {
+    if (a->out_dim == a->hidden) mode = M_VEC;
+    else if (a->out_dim <= 32 && !a->use_ln) mode = M_NOUT;
+  }
+  const bool vec = mode == M_VEC;
   agn_mlp_bwd_args* am = const_cast<agn_mlp_bwd_args*>(a);
   if (res_bwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
@@ -949,7 +1025,7 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
   }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));
   am->ln_rows = (int)grid.x;
-  AGN_DISPATCH(mlp_bwd_kernel);
+  AGN_DISPATCH(AGN_BWD_MODES);
   return launch_status();
 }
 
