@@ -313,6 +313,9 @@ class GMPFn(torch.autograd.Function):
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
         ctx.save_for_backward(x, e)
+        # an unused e' (the U-Net restores fine edges from the skip, bsms_mgn.py:203) arrives as
+        # None instead of a materialised [E,H] zero tensor; the kernels read it as zero
+        ctx.set_materialize_grads(False)
         return x_out, e_out
 
     @staticmethod
@@ -323,7 +326,8 @@ class GMPFn(torch.autograd.Function):
         es, ns = spec.edge, spec.node
         dt, dev = x.dtype, x.device
         N, E, H = x.shape[0], e.shape[0], spec.H
-        gx, ge = _c(gx), _c(ge)
+        gx = _c(gx) if gx is not None else torch.zeros_like(x)
+        ge = _c(ge) if ge is not None else None
         # ---- NodeBlock: d(x), d(agg)
         gpre_n = [torch.empty(N, H, dtype=dt, device=dev) for _ in range(ns.nlin)]
         dx = torch.empty_like(x)
@@ -384,13 +388,52 @@ class GMPFn(torch.autograd.Function):
 
 
 # --------------------------------------------------------------------------- pooling
+class GradBox:
+    """Side channel for a U-Net skip tensor's up-path gradient (bsms_mgn.py:196-206).
+
+    A skip tensor has two consumers: the pooling of the down path and the up path (skip add /
+    restored fine edges). Autograd would sum their gradients with a separate [rows, H] add; here
+    the up-path consumer parks its gradient in the box (returning None to autograd) and the
+    pooling backward — which the graph orders after it — adds it inside its gather kernel.
+    """
+    __slots__ = ("g", "armed")
+
+    def __init__(self):
+        self.g = None
+        self.armed = False
+
+    def put(self, g):
+        self.g = g if self.g is None else self.g + g
+
+    def take(self):
+        if self.armed and self.g is None:
+            raise RuntimeError("aerognn: skip gradient missing (autograd order violated)")
+        g, self.g = self.g, None
+        return g
+
+
+class SkipFn(torch.autograd.Function):
+    """Identity for a skip tensor re-used on the up path; its gradient goes to `box`."""
+
+    @staticmethod
+    def forward(ctx, t, box):
+        box.armed = True
+        ctx.box = box
+        return t.view_as(t)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.box.put(g)
+        return None, None
+
+
 class PoolNodeFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, pool):
+    def forward(ctx, x, pool, box=None):
         x = _c(x)
         out = torch.empty(pool.nc, x.shape[1], dtype=x.dtype, device=x.device)
         segment_sum(pool.nc, x.shape[1], pool.c2f_ptr, pool.c2f, x, out, mean=True)
-        ctx.pool = pool
+        ctx.pool, ctx.box = pool, box
         ctx.n = x.shape[0]
         return out
 
@@ -398,19 +441,20 @@ class PoolNodeFn(torch.autograd.Function):
     def backward(ctx, g):
         p = ctx.pool
         g = _c(g)
+        add = ctx.box.take() if ctx.box is not None else None
         dx = torch.empty(ctx.n, g.shape[1], dtype=g.dtype, device=g.device)
-        gather_rows(ctx.n, g.shape[1], p.f2c, g, dx, cnt_ptr=p.c2f_ptr)
-        return dx, None
+        gather_rows(ctx.n, g.shape[1], p.f2c, g, dx, cnt_ptr=p.c2f_ptr, add=_c(add) if add is not None else None)
+        return dx, None, None
 
 
 class PoolEdgeFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, e, pool):
+    def forward(ctx, e, pool, box=None):
         e = _c(e)
         ec = pool.coarse.E
         out = torch.empty(ec, e.shape[1], dtype=e.dtype, device=e.device)
         segment_sum(ec, e.shape[1], pool.cmem_ptr, pool.cand_sorted, e, out, mean=True)
-        ctx.pool = pool
+        ctx.pool, ctx.box = pool, box
         ctx.n = e.shape[0]
         return out
 
@@ -418,19 +462,25 @@ class PoolEdgeFn(torch.autograd.Function):
     def backward(ctx, g):
         p = ctx.pool
         g = _c(g)
+        add = ctx.box.take() if ctx.box is not None else None
         de = torch.empty(ctx.n, g.shape[1], dtype=g.dtype, device=g.device)
-        gather_rows(ctx.n, g.shape[1], p.inv, g, de, cnt_ptr=p.cmem_ptr)
-        return de, None
+        gather_rows(ctx.n, g.shape[1], p.inv, g, de, cnt_ptr=p.cmem_ptr, add=_c(add) if add is not None else None)
+        return de, None, None
 
 
 class UnpoolFn(torch.autograd.Function):
+    """x_fine = coarse[f2c] + skip (bsms_mgn.py:199-200, 303-306). With `box`, the skip's
+    gradient (the identity) is parked for the matching PoolNodeFn backward."""
+
     @staticmethod
-    def forward(ctx, coarse, skip, pool):
+    def forward(ctx, coarse, skip, pool, box=None):
         coarse, skip = _c(coarse), _c(skip)
         n = skip.shape[0]
         out = torch.empty_like(skip)
         gather_rows(n, skip.shape[1], pool.f2c, coarse, out, add=skip)
-        ctx.pool = pool
+        ctx.pool, ctx.box = pool, box
+        if box is not None:
+            box.armed = True
         return out
 
     @staticmethod
@@ -439,7 +489,10 @@ class UnpoolFn(torch.autograd.Function):
         g = _c(g)
         dc = torch.empty(p.nc, g.shape[1], dtype=g.dtype, device=g.device)
         segment_sum(p.nc, g.shape[1], p.c2f_ptr, p.c2f, g, dc)
-        return dc, g, None
+        if ctx.box is not None:
+            ctx.box.put(g)
+            return dc, None, None, None
+        return dc, g, None, None
 
 
 # --------------------------------------------------------------------------- standalone blocks

@@ -323,14 +323,14 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
 // ------------------------------------------------------------------------- backward
 template <typename T, int NR, int MODE>
 AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
-  const T* g1 = reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim;
+  const T* g1 = a.g ? reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim : nullptr;
   const T* g2 = a.g2 ? reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim : nullptr;
   if constexpr (MODE == M_NOUT) {  // out_dim <= 32: acc tile 0 only
 #pragma unroll
     for (int i = 0; i < NR; ++i) g[i] = 0.f;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f32x4 x = load4_masked(g1, 8 * q + 4 * h, a.out_dim, false);
+      f32x4 x = g1 ? load4_masked(g1, 8 * q + 4 * h, a.out_dim, false) : f32x4{0.f, 0.f, 0.f, 0.f};
       if (g2) {
         const f32x4 y = load4_masked(g2, 8 * q + 4 * h, a.out_dim, false);
         x[0] += y[0]; x[1] += y[1]; x[2] += y[2]; x[3] += y[3];
@@ -338,7 +338,12 @@ AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool v
       g[4 * q] = x[0]; g[4 * q + 1] = x[1]; g[4 * q + 2] = x[2]; g[4 * q + 3] = x[3];
     }
   } else {
-    load_row<T, NR, MODE == M_VEC>(g, g1, a.out_dim, h);
+    if (g1) {
+      load_row<T, NR, MODE == M_VEC>(g, g1, a.out_dim, h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) g[i] = 0.f;
+    }
     if (g2) add_row<T, NR, MODE == M_VEC>(g, g2, a.out_dim, h);
   }
   if (!valid) {
@@ -638,7 +643,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 
 template <typename T, int NR>
 AGN_DEV void load_grad_w(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool valid, int h) {
-  load_row_w<T, NR>(g, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, h);
+  if (a.g) {
+    load_row_w<T, NR>(g, reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim, h);
+  } else {  // unused output: zero incoming gradient (no materialised zeros)
+#pragma unroll
+    for (int i = 0; i < NR; ++i) g[i] = 0.f;
+  }
   if (a.g2) add_row_w<T, NR>(g, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
   if (!valid) {
 #pragma unroll
@@ -650,8 +660,9 @@ template <typename T, int NR>
 AGN_DEV void add_grad_w(float (&v)[NR], const agn_mlp_bwd_args& a, int rr, int h) {
   // v += (g + g2): the incoming gradient is summed first, as autograd accumulates it
   const T* g = reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim;
-  if (!a.g2) {
-    add_row_w<T, NR>(v, g, h);
+  if (!a.g2 || !a.g) {
+    if (a.g) add_row_w<T, NR>(v, g, h);
+    else if (a.g2) add_row_w<T, NR>(v, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
     return;
   }
   const T* g2 = reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim;

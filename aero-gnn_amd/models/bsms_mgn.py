@@ -9,7 +9,7 @@ fused GMP layers, mean-pool / unpool+skip kernels, and the decoder.
 import torch
 from torch import nn
 
-from aerognn.functions import PoolEdgeFn, PoolNodeFn, UnpoolFn
+from aerognn.functions import GradBox, PoolEdgeFn, PoolNodeFn, SkipFn, UnpoolFn
 from aerognn.graph import Level, downsample_maps
 from aerognn.core import require_device, segment_sum
 from models.mlp import MLP
@@ -106,18 +106,20 @@ class BiStridedMeshGraphNet(nn.Module):
         for scale_idx, layers in enumerate(self.down_layers):
             for layer in layers:
                 cn, ce = layer.forward_level(cn, ce, lv)
-            skips.append((cn, ce, lv))
+            boxes = (GradBox(), GradBox()) if torch.is_grad_enabled() else (None, None)
+            skips.append((cn, ce, lv, boxes))
             P = pools[scale_idx]
-            cn = PoolNodeFn.apply(cn, P)
-            ce = PoolEdgeFn.apply(ce, P)
+            cn = PoolNodeFn.apply(cn, P, boxes[0])
+            ce = PoolEdgeFn.apply(ce, P, boxes[1])
             lv = P.coarse
         for layer in self.bottleneck_layers:
             cn, ce = layer.forward_level(cn, ce, lv)
         for scale_idx, layers in enumerate(self.up_layers):
             if pools:
-                sn, se, slv = skips[-(scale_idx + 1)]
-                cn = UnpoolFn.apply(cn, sn, pools[-(scale_idx + 1)])   # coarse[f2c] + skip
-                ce, lv = se, slv                                        # fine edges restored
+                sn, se, slv, (bn, be) = skips[-(scale_idx + 1)]
+                cn = UnpoolFn.apply(cn, sn, pools[-(scale_idx + 1)], bn)  # coarse[f2c] + skip
+                ce = SkipFn.apply(se, be) if be is not None else se      # fine edges restored
+                lv = slv
             for layer in layers:
                 cn, ce = layer.forward_level(cn, ce, lv)
         return self.decoder(cn)

@@ -94,7 +94,8 @@ typedef struct {
   const void* hpre;
   const float* stats;
   const float* ln_g;
-  /* upstream gradient of the MLP output (+ optional gathered add: g2[gidx[r]]) */
+  /* upstream gradient of the MLP output (+ optional gathered add: g2[gidx[r]]);
+   * g = NULL means a zero gradient (an output autograd left unused) */
   const void* g;
   const void* g2;
   const int32_t* gidx;
