@@ -62,6 +62,15 @@ class WgradBatch(C.Structure):
     _fields_ = [("n", i32), ("_pad", i32), ("d", WgradDesc * MAX_WGRAD)]
 
 
+class WecArgs(C.Structure):
+    _fields_ = [("n", i32), ("e", i32), ("dtype", i32), ("out_dim", i32), ("hid", i32), ("pos_dim", i32),
+                ("pos_ld", i32), ("mean", i32),
+                ("rowptr", vp), ("src", vp), ("dst", vp), ("perm", vp), ("rowptr_src", vp), ("perm_src", vp),
+                ("pos", vp), ("pab", vp), ("tx", vp), ("w1c", vp), ("w2", vp),
+                ("w_in", vp), ("w_out", vp), ("out", vp), ("dout", vp), ("gw", vp), ("s_csc", vp), ("dh", vp),
+                ("dpa", vp), ("dpb", vp), ("dtx", vp), ("dw_in", vp), ("partial", vp)]
+
+
 class PackDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
                 ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
@@ -111,6 +120,18 @@ def lib():
             "agn_pool_edge_candidates": (i32, [i32, vp, vp, vp, vp, vp]),
             "agn_pool_edge_sort": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
             "agn_pool_edge_emit": (i32, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp]),
+            "agn_bfs_work_ints": (C.c_size_t, [i32]),
+            "agn_bfs_distance": (i32, [vp, vp, i32, i32, vp, vp, C.POINTER(i32), vp]),
+            "agn_center_seed": (i32, [vp, i32, i32, i32, vp, vp]),
+            "agn_maxdeg_seed": (i32, [vp, i32, vp, vp]),
+            "agn_compact_work_ints": (C.c_size_t, [i32]),
+            "agn_bistride_select": (i32, [vp, i32, vp, C.POINTER(i32), vp, vp]),
+            "agn_index_map": (i32, [vp, i32, i32, vp, vp]),
+            "agn_subgraph_edges": (i32, [vp, vp, i32, vp, vp, vp, C.POINTER(i32), vp, vp]),
+            "agn_scatter_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
+            "agn_wec_blocks": (i32, [i32]),
+            "agn_wec_forward": (i32, [C.POINTER(WecArgs), vp]),
+            "agn_wec_backward": (i32, [C.POINTER(WecArgs), vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -127,7 +127,7 @@ class Pack:
             o, nb = offs[key]
             self.views[key] = base + o
             for (v, off) in parts:
-                descs.append(L.PackDesc(v.data_ptr(), base + o, dt_code(v.dtype), L.F32, 0, v.numel(), 0, 1,
+                descs.append(L.PackDesc(v.data_ptr(), base + o, dt_code(v.dtype), L.F32, 0, v.numel(), 0, v.stride(0),
                                         0, int(off), 0, n))
                 maxthr = max(maxthr, v.numel())
         raw = (L.PackDesc * len(descs))(*descs)
@@ -139,8 +139,8 @@ class Pack:
     def update(self, dtype, device):
         for key, (M, K, parts) in self.mats.items():
             for p in parts:
-                if not p[0].is_contiguous():
-                    raise RuntimeError("aerognn: packed weights must be contiguous")
+                if p[0].dim() != 2 or p[0].stride(1) != 1:
+                    raise RuntimeError("aerognn: packed weights need unit column stride (rows may be strided)")
         sig = self._signature(dtype)
         if sig != self._sig:
             self._build(dtype, device)
@@ -224,6 +224,13 @@ def gather_rows(rows, k, idx, src, out, cnt_ptr=None, add=None):
     check(L.lib().agn_gather_rows(rows, k, dt_code(src.dtype), ptr(idx), ptr(src), src.stride(0),
                                   ptr(cnt_ptr), ptr(add), add.stride(0) if add is not None else 0,
                                   ptr(out), out.stride(0), stream()), "gather_rows")
+    return out
+
+
+def scatter_rows(idx32, src, out):
+    """out[idx[r]] = src[r] (rows of `src` in order; idx unique)."""
+    check(L.lib().agn_scatter_rows(idx32.numel(), src.shape[1], dt_code(src.dtype), ptr(idx32), ptr(src),
+                                   src.stride(0), ptr(out), out.stride(0), stream()), "scatter_rows")
     return out
 
 

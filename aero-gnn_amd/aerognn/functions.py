@@ -5,6 +5,9 @@
   PoolNodeFn   bsms_mgn.py:265-267 scatter_mean of node latents (and pos)
   PoolEdgeFn   bsms_mgn.py:283     scatter_mean of edge latents over coalesced edges
   UnpoolFn     bsms_mgn.py:199-200,303-306 coarse[f2c] + skip
+  GradBox/SkipFn  skip-gradient side channel of the U-Net (no autograd adds)
+  GatherRowsFn / UnpoolRowsFn / WECFn / WECGivenFn  the stale BSMS-GNN ops:
+               x[node_indices], Unpool, WeightedEdgeConv with computed / given weights
 
 Forward kernels write the activations the backward needs (relu outputs, pre-LN outputs and
 LN statistics); backward kernels run the chain rule per row on MFMA and the weight
@@ -12,12 +15,15 @@ gradients are G^T X products accumulated in fp32.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _lib as L
+from ._lib import check, ptr
 from .core import (Pack, WGrad, bwd_nblocks, colsum_rows, cost_edge_bwd, cost_edge_fwd, cost_node_bwd,
-                   cost_node_fwd, cost_proj, gather_rows, mlp_backward, mlp_forward, require_device,
-                   segment_sum)
+                   cost_node_fwd, cost_proj, dt_code, gather_rows, mlp_backward, mlp_forward, require_device,
+                   scatter_rows, segment_sum, stream)
 
 
 def _c(t):
@@ -203,6 +209,7 @@ class LayerSpec:
         self.pack = Pack()
         self.edge = self.node = None
         self.trick = False
+        self.gmp_order = False  # GMP (bistride_ops @235) concatenates [x_src, x_dst, e]
         self.aggregation = "add"
         H = None
         if node_block is not None:
@@ -253,6 +260,31 @@ class LayerSpec:
         if node_block is not None and node_block.mlp.activation_fn != "relu":
             raise NotImplementedError("aerognn kernels implement ReLU MLPs (config.yaml activation_fn)")
 
+    @classmethod
+    def from_gmp(cls, gmp):
+        """GMP of the stale BSMS-GNN design (bistride_ops @216-250): edge_mlp / node_mlp =
+        Sequential(Linear, act, Linear, LayerNorm), edge input cat[x_src, x_dst, e]."""
+        self = cls.__new__(cls)
+        self.pack = Pack()
+        self.trick, self.gmp_order, self.aggregation = False, True, "add"
+        if not isinstance(gmp.edge_mlp[1], torch.nn.ReLU):
+            raise NotImplementedError("aerognn kernels implement ReLU MLPs (GMP activation='relu')")
+        e0, e2, eln = gmp.edge_mlp[0], gmp.edge_mlp[2], gmp.edge_mlp[3]
+        n0, n2, nln = gmp.node_mlp[0], gmp.node_mlp[2], gmp.node_mlp[3]
+        H = e0.weight.shape[0]
+        if H not in (32, 64, 128):
+            raise NotImplementedError(f"aerognn kernels support hidden 32/64/128, got {H}")
+        self.edge = ChainSpec([(e0.weight, e0.bias), (e2.weight, e2.bias)], (eln.weight, eln.bias), H, self.pack, "e")
+        self.node = ChainSpec([(n0.weight, n0.bias), (n2.weight, n2.bias)], (nln.weight, nln.bias), H, self.pack, "n")
+        self.H = H
+        for c in (self.edge, self.node):
+            c.check_hidden()
+            if c.out_dim != H:
+                raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
+        if self.node.in_dim != 2 * H or self.edge.in_dim != 3 * H:
+            raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
+        return self
+
     def edge_params(self):
         if self.edge is None:
             return []
@@ -296,10 +328,11 @@ class GMPFn(torch.autograd.Function):
                         resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
                         tag="edge_fwd", cost=cost_edge_fwd(E, N, H, sz, es.nlin, train))
         else:
+            se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
+            ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
+            sd = (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
-                        segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None),
-                              (L.SEG_GATHER, H, x.stride(0), x, level.src, None),
-                              (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)],
+                        segs=[ss, sd, se] if spec.gmp_order else [se, ss, sd],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), resid=e, out=e_out,
                         acts=ea, hpre=ehp, stats=est)
         agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
@@ -350,7 +383,8 @@ class GMPFn(torch.autograd.Function):
         else:
             dxs = torch.empty(E, H, dtype=dt, device=dev)
             dxd = torch.empty(E, H, dtype=dt, device=dev)
-            din = [(H, de, True), (H, dxs, False), (H, dxd, False)]
+            din = [(H, dxs, False), (H, dxd, False), (H, de, True)] if spec.gmp_order else \
+                [(H, de, True), (H, dxs, False), (H, dxd, False)]
         nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
                      hpre=ehp, stats=est, din=din, ln_partial=part_e,
@@ -382,7 +416,8 @@ class GMPFn(torch.autograd.Function):
             dx = dx + ds + dd
             xs = x.index_select(0, lv.src.long())
             xd = x.index_select(0, lv.dst.long())
-            grads_edge = _chain_param_grads(es, gpre_e, [e, xs, xd], ea, part_e, nb_e)
+            grads_edge = _chain_param_grads(es, gpre_e, [xs, xd, e] if spec.gmp_order else [e, xs, xd],
+                                            ea, part_e, nb_e)
         grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n)
         return (dx, de, None, None, None, *grads_edge, *grads_node)
 
@@ -619,3 +654,210 @@ class NodeBlockFn(torch.autograd.Function):
         gather_rows(E, H, lv.dst, dagg, de, cnt_ptr=lv.rowptr if spec.aggregation == "mean" else None)
         grads = _chain_param_grads(ns, gpre, [x, agg], na, part, nb)
         return (dx, de, None, None, None, *grads)
+
+
+# --------------------------------------------------------------------------- BSMS-GNN (stale design)
+class GatherRowsFn(torch.autograd.Function):
+    """y = x[idx] (old bsms_mgn @145: x = x[node_indices[i]]); idx unique. Backward scatters."""
+
+    @staticmethod
+    def forward(ctx, x, idx32):
+        x = _c(x)
+        out = torch.empty(idx32.numel(), x.shape[1], dtype=x.dtype, device=x.device)
+        gather_rows(idx32.numel(), x.shape[1], idx32, x, out)
+        ctx.idx, ctx.n = idx32, x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        dx = torch.zeros(ctx.n, g.shape[1], dtype=g.dtype, device=g.device)
+        scatter_rows(ctx.idx, g, dx)
+        return dx, None
+
+
+class UnpoolRowsFn(torch.autograd.Function):
+    """Unpool.forward (bistride_ops @102): zeros[n_fine, C]; x_fine[indices] = x_coarse."""
+
+    @staticmethod
+    def forward(ctx, xc, idx32, n_fine):
+        xc = _c(xc)
+        out = torch.zeros(n_fine, xc.shape[1], dtype=xc.dtype, device=xc.device)
+        scatter_rows(idx32, xc, out)
+        ctx.idx = idx32
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        dxc = torch.empty(ctx.idx.numel(), g.shape[1], dtype=g.dtype, device=g.device)
+        gather_rows(ctx.idx.numel(), g.shape[1], ctx.idx, g, dxc)
+        return dxc, None, None
+
+
+class WecSpec:
+    """Packed operands of a WeightedEdgeConv (bistride_ops @136): transform T [out, in] (+b_T),
+    edge_weight_mlp = Linear(2 in + 1, 64) -> ReLU -> Linear(64, 1) -> Sigmoid."""
+
+    HID = 64
+
+    def __init__(self, mod):
+        T, W1, W2 = mod.transform, mod.edge_weight_mlp[0], mod.edge_weight_mlp[2]
+        self.inp, self.out = T.weight.shape[1], T.weight.shape[0]
+        i, o, hd = self.inp, self.out, self.HID
+        if i not in (32, 64, 128) or o not in (64, 128) or W1.weight.shape[0] != hd:
+            raise NotImplementedError("aerognn WeightedEdgeConv: in_dim 32/64/128, out_dim 64/128, hidden 64")
+        self.mod = mod
+        p = self.pack = Pack()
+        p.matrix("T", o, i, [(T.weight, 0, 0, False)])
+        p.vector("Tb", o, [(T.bias, 0)])
+        p.matrix("W1", 2 * hd, i, [(W1.weight[:, :i], 0, 0, False), (W1.weight[:, i:2 * i], hd, 0, False)])
+        p.vector("W1b", 2 * hd, [(W1.bias, hd)])
+        p.vector("w1c", hd, [(W1.weight[:, 2 * i], 0)])
+        p.vector("w2", hd + 1, [(W2.weight[0], 0), (W2.bias, hd)])
+        p.matrix("back", i, o + 2 * hd, [(T.weight, 0, 0, True), (W1.weight[:, :i], 0, o, True),
+                                         (W1.weight[:, i:2 * i], 0, o + hd, True)])
+        p.matrix("backT", i, o, [(T.weight, 0, 0, True)])
+
+    def params(self):
+        m = self.mod
+        return [m.edge_weight_mlp[0].weight, m.edge_weight_mlp[0].bias, m.edge_weight_mlp[2].weight,
+                m.edge_weight_mlp[2].bias, m.transform.weight, m.transform.bias]
+
+
+def _wec_args(spec, x, level, mean):
+    a = L.WecArgs()
+    a.n, a.e, a.dtype = x.shape[0], level.E, dt_code(x.dtype)
+    a.out_dim, a.hid, a.mean = spec.out, WecSpec.HID, int(mean)
+    a.rowptr, a.src, a.dst, a.perm = ptr(level.rowptr), ptr(level.src), ptr(level.dst), ptr(level.perm)
+    a.rowptr_src, a.perm_src = ptr(level.rowptr_src), ptr(level.perm_src)
+    return a
+
+
+def _wec_tx(spec, x):
+    tx = torch.empty(x.shape[0], spec.out, dtype=x.dtype, device=x.device)
+    mlp_forward(rows=x.shape[0], dtype=x.dtype, hidden=spec.inp, nlin=1, out_dim=spec.out,
+                segs=[(L.SEG_PLAIN, spec.inp, x.stride(0), x, None, None)],
+                wpk=[spec.pack["T"]], bias=[spec.pack["Tb"]], out=tx)
+    return tx
+
+
+class WECFn(torch.autograd.Function):
+    """WeightedEdgeConv with computed weights (bistride_ops @152-210) -> (out, w [E,1])."""
+
+    @staticmethod
+    def forward(ctx, x, pos, level, spec, mean, *params):
+        require_device(x, pos)
+        x = _c(x)
+        dt, dev = x.dtype, x.device
+        N, E, hd = x.shape[0], level.E, WecSpec.HID
+        spec.pack.update(dt, dev)
+        pab = torch.empty(N, 2 * hd, dtype=dt, device=dev)
+        mlp_forward(rows=N, dtype=dt, hidden=spec.inp, nlin=1, out_dim=2 * hd,
+                    segs=[(L.SEG_PLAIN, spec.inp, x.stride(0), x, None, None)],
+                    wpk=[spec.pack["W1"]], bias=[spec.pack["W1b"]], out=pab)
+        tx = _wec_tx(spec, x)
+        pos32 = pos.float().contiguous()
+        w = torch.empty(E, 1, dtype=dt, device=dev)
+        out = torch.empty(N, spec.out, dtype=dt, device=dev)
+        a = _wec_args(spec, x, level, mean)
+        a.pos_dim, a.pos_ld, a.pos = pos32.shape[1], pos32.stride(0), ptr(pos32)
+        a.pab, a.tx, a.w1c, a.w2 = ptr(pab), ptr(tx), spec.pack["w1c"], spec.pack["w2"]
+        a.w_out, a.out = ptr(w), ptr(out)
+        check(L.lib().agn_wec_forward(C.byref(a), stream()), "wec_forward")
+        ctx.spec, ctx.level, ctx.mean = spec, level, mean
+        ctx.save_for_backward(x, pos32, pab, tx)
+        ctx.set_materialize_grads(False)
+        return out, w
+
+    @staticmethod
+    def backward(ctx, dout, dw):
+        x, pos32, pab, tx = ctx.saved_tensors
+        spec, level = ctx.spec, ctx.level
+        dt, dev = x.dtype, x.device
+        N, E, hd = x.shape[0], level.E, WecSpec.HID
+        if dout is None:
+            dout = torch.zeros(N, spec.out, dtype=dt, device=dev)
+        dout = _c(dout)
+        s_csc = torch.empty(E, dtype=torch.float32, device=dev)
+        dh = torch.empty(E, hd, dtype=torch.float32, device=dev)
+        dpa = torch.empty(N, hd, dtype=dt, device=dev)
+        dpb = torch.empty(N, hd, dtype=dt, device=dev)
+        dtx = torch.empty(N, spec.out, dtype=dt, device=dev)
+        nblk = int(L.lib().agn_wec_blocks(N))
+        partial = torch.empty(max(nblk, 1), 2 * hd + 1, dtype=torch.float32, device=dev)
+        a = _wec_args(spec, x, level, ctx.mean)
+        a.pos_dim, a.pos_ld, a.pos = pos32.shape[1], pos32.stride(0), ptr(pos32)
+        a.pab, a.tx, a.w1c, a.w2 = ptr(pab), ptr(tx), spec.pack["w1c"], spec.pack["w2"]
+        dw = _c(dw) if dw is not None else None
+        a.dout, a.gw = ptr(dout), ptr(dw)
+        a.s_csc, a.dh, a.dpa, a.dpb, a.dtx, a.partial = ptr(s_csc), ptr(dh), ptr(dpa), ptr(dpb), ptr(dtx), ptr(partial)
+        check(L.lib().agn_wec_backward(C.byref(a), stream()), "wec_backward")
+        i, o = spec.inp, spec.out
+        dx = torch.empty_like(x)
+        mlp_forward(rows=N, dtype=dt, hidden=i, nlin=1, out_dim=i,
+                    segs=[(L.SEG_PLAIN, o, o, dtx, None, None), (L.SEG_PLAIN, hd, hd, dpa, None, None),
+                          (L.SEG_PLAIN, hd, hd, dpb, None, None)],
+                    wpk=[spec.pack["back"]], bias=[None], out=dx)
+        W1 = spec.mod.edge_weight_mlp[0].weight
+        dW1 = torch.empty(hd, 2 * i + 1, dtype=torch.float32, device=dev)
+        db1 = torch.empty(hd, dtype=torch.float32, device=dev)
+        dT = torch.empty(o, i, dtype=torch.float32, device=dev)
+        dTb = torch.empty(o, dtype=torch.float32, device=dev)
+        wg = WGrad()
+        wg.add(dtx, x, dT, dTb)
+        wg.add(dpa, x, dW1[:, :i])
+        wg.add(dpb, x, dW1[:, i:2 * i], db1)
+        wg.run()
+        red = torch.empty(2 * hd + 1, dtype=torch.float32, device=dev)
+        colsum_rows(partial, nblk, 2 * hd + 1, red)
+        dW1[:, 2 * i].copy_(red[hd:2 * hd])
+        ps = spec.params()
+        grads = [dW1, db1, red[:hd].view(1, hd), red[2 * hd:], dT, dTb]
+        grads = [g.to(p.dtype) for g, p in zip(grads, ps)]
+        return (dx, None, None, None, None, *grads)
+
+
+class WECGivenFn(torch.autograd.Function):
+    """WeightedEdgeConv with given weights (compute_weights=False, bistride_ops @173)."""
+
+    @staticmethod
+    def forward(ctx, x, w, level, spec, mean, *params):
+        require_device(x, w)
+        x = _c(x)
+        dt, dev = x.dtype, x.device
+        spec.pack.update(dt, dev)
+        w = _c(w.to(dt))
+        tx = _wec_tx(spec, x)
+        out = torch.empty(x.shape[0], spec.out, dtype=dt, device=dev)
+        a = _wec_args(spec, x, level, mean)
+        a.tx, a.w_in, a.out = ptr(tx), ptr(w), ptr(out)
+        check(L.lib().agn_wec_forward(C.byref(a), stream()), "wec_forward")
+        ctx.spec, ctx.level, ctx.mean = spec, level, mean
+        ctx.save_for_backward(x, w, tx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, tx = ctx.saved_tensors
+        spec, level = ctx.spec, ctx.level
+        dt, dev = x.dtype, x.device
+        N, E = x.shape[0], level.E
+        dout = _c(dout)
+        s_csc = torch.empty(E, dtype=torch.float32, device=dev)
+        dtx = torch.empty(N, spec.out, dtype=dt, device=dev)
+        dw = torch.empty(E, 1, dtype=dt, device=dev) if ctx.needs_input_grad[1] else None
+        a = _wec_args(spec, x, level, ctx.mean)
+        a.tx, a.w_in, a.dout, a.s_csc, a.dtx, a.dw_in = ptr(tx), ptr(w), ptr(dout), ptr(s_csc), ptr(dtx), ptr(dw)
+        check(L.lib().agn_wec_backward(C.byref(a), stream()), "wec_backward")
+        dx = torch.empty_like(x)
+        mlp_forward(rows=N, dtype=dt, hidden=spec.inp, nlin=1, out_dim=spec.inp,
+                    segs=[(L.SEG_PLAIN, spec.out, spec.out, dtx, None, None)],
+                    wpk=[spec.pack["backT"]], bias=[None], out=dx)
+        dT = torch.empty(spec.out, spec.inp, dtype=torch.float32, device=dev)
+        dTb = torch.empty(spec.out, dtype=torch.float32, device=dev)
+        wg = WGrad()
+        wg.add(dtx, x, dT, dTb)
+        wg.run()
+        T = spec.mod.transform
+        return (dx, dw, None, None, None, dT.to(T.weight.dtype), dTb.to(T.bias.dtype))

@@ -810,7 +810,7 @@ template <typename S>
 AGN_DEV void pack_one(const agn_pack_desc& d, int tid) {
   const S* w = reinterpret_cast<const S*>(d.src);
   if (d.rows == 0) {  // vector -> fp32
-    if (tid < d.cols) reinterpret_cast<float*>(d.dst)[d.col_off + tid] = to_f(w[tid]);
+    if (tid < d.cols) reinterpret_cast<float*>(d.dst)[d.col_off + tid] = to_f(w[(size_t)tid * d.ld]);
     return;
   }
   const int OT = (d.rows + 31) / 32;

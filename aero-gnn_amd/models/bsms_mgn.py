@@ -142,3 +142,118 @@ class BiStridedMeshGraphNet(nn.Module):
 
     def _unpool_nodes(self, coarse_nodes: torch.Tensor, assignment: torch.Tensor) -> torch.Tensor:
         return coarse_nodes[assignment]
+
+
+# =====================================================================================
+# The earlier BSMS-GNN design of this module (stale bytecode bsms_mgn.cpython-311.pyc,
+# "bm@L" = its source line L; semantics in SURVEY Appendix A): BFS bi-stride hierarchy built
+# once per mesh (MultiScaleGraphPreprocessor), U-Net of GMP layers with WeightedEdgeConv
+# pooling and Unpool (BSMSGMP), and the full model (BSMS_MeshGraphNet). Parity unpinned: the
+# bytecode cannot be executed; tests check against oracle/bsmsgnn.py (restated from Appendix A).
+# =====================================================================================
+from aerognn import bistride as _bistride  # noqa: E402
+from aerognn.functions import GatherRowsFn  # noqa: E402
+from models.bistride_ops import GMP, Unpool, WeightedEdgeConv, _level_of  # noqa: E402
+
+
+class MultiScaleGraphPreprocessor:
+    """bm@20: multi-scale hierarchy by bistride pooling, built once per mesh (on the GPU)."""
+
+    def __init__(self, num_levels):
+        self.num_levels = num_levels
+
+    def create_multiscale_graph(self, data):
+        """bm@32: data has edge_index and pos (PyG Data). Returns {'edge_indices', 'node_indices',
+        'num_nodes', 'positions'}: per-level lists (edge_indices/num_nodes/positions have
+        num_levels + 1 entries, node_indices num_levels)."""
+        ei = data.edge_index
+        pos = getattr(data, "pos", None)
+        n = getattr(data, "num_nodes", None)
+        if n is None:
+            n = data.x.size(0)
+        require_device(ei, pos)
+        return _bistride.create_multiscale_graph(ei, pos, int(n), self.num_levels)
+
+
+class BSMSGMP(nn.Module):
+    """bm@86-201: down path GMP -> WeightedEdgeConv (weights computed) -> x[selected]; bottom GMP;
+    up path Unpool -> WeightedEdgeConv (down-path weights) -> + skip."""
+
+    def __init__(self, num_levels, latent_dim, hidden_dim, pos_dim=2):
+        super().__init__()
+        self.num_levels = num_levels
+        self.latent_dim = latent_dim
+        self.hidden_dim = hidden_dim
+        self.pos_dim = pos_dim
+        self.down_gmps = nn.ModuleList([GMP(latent_dim, latent_dim, hidden_dim) for _ in range(num_levels + 1)])
+        self.down_edge_convs = nn.ModuleList([WeightedEdgeConv(latent_dim, latent_dim, aggr='add')
+                                              for _ in range(num_levels)])
+        self.bottom_gmp = GMP(latent_dim, latent_dim, hidden_dim)
+        self.up_edge_convs = nn.ModuleList([WeightedEdgeConv(latent_dim, latent_dim, aggr='add')
+                                            for _ in range(num_levels)])
+        self.unpools = nn.ModuleList([Unpool() for _ in range(num_levels)])
+
+    def forward(self, x, edge_attrs, edge_indices, node_indices, num_nodes_list, positions):
+        L = self.num_levels
+        cache = {}
+        lvs = [_level_of(edge_indices[i], int(num_nodes_list[i]), cache) for i in range(L + 1)]
+        # edge latents stay in each level's CSC order inside the U-Net (only x is returned)
+        eas = [ea.index_select(0, lv.perm) for ea, lv in zip(edge_attrs, lvs)]
+        skips, weights = [], []
+        for i in range(L):
+            x, eas[i] = self.down_gmps[i].forward_level(x, eas[i], lvs[i])
+            skips.append(x)
+            xc, w = self.down_edge_convs[i](x, edge_indices[i], positions[i], compute_weights=True, level=lvs[i])
+            weights.append(w)
+            x = x + xc
+            x = GatherRowsFn.apply(x, node_indices[i].to(torch.int32).contiguous())
+        x, eas[L] = self.bottom_gmp.forward_level(x, eas[L], lvs[L])
+        for i in range(L - 1, -1, -1):
+            x = self.unpools[i](x, node_indices[i], num_nodes_list[i])
+            xc, _ = self.up_edge_convs[i](x, edge_indices[i], positions[i], edge_weights=weights[i],
+                                          compute_weights=False, level=lvs[i])
+            x = x + xc + skips[i]
+        return x
+
+
+class BSMS_MeshGraphNet(nn.Module):
+    """bm@204-300: MLP encoders (LayerNorm), BSMSGMP processor, MLP decoder (no LayerNorm)."""
+
+    def __init__(self, input_node_dim, input_edge_dim, output_node_dim, num_levels=3, latent_dim=128,
+                 hidden_dim=128, pos_dim=2, num_hidden_layers_encoder=2, num_hidden_layers_decoder=2,
+                 activation_fn='relu', dropout=0.0):
+        super().__init__()
+        self.num_levels = num_levels
+        self.latent_dim = latent_dim
+        self.node_encoder = MLP(input_dim=input_node_dim, hidden_dim=hidden_dim, output_dim=latent_dim,
+                                num_hidden_layers=num_hidden_layers_encoder, activation_fn=activation_fn,
+                                dropout=dropout, use_layer_norm=True)
+        self.edge_encoder = MLP(input_dim=input_edge_dim, hidden_dim=hidden_dim, output_dim=latent_dim,
+                                num_hidden_layers=num_hidden_layers_encoder, activation_fn=activation_fn,
+                                dropout=dropout, use_layer_norm=True)
+        self.bsgmp = BSMSGMP(num_levels, latent_dim, hidden_dim, pos_dim)
+        self.decoder = MLP(input_dim=latent_dim, hidden_dim=hidden_dim, output_dim=output_node_dim,
+                           num_hidden_layers=num_hidden_layers_decoder, activation_fn=activation_fn,
+                           dropout=dropout, use_layer_norm=False)
+
+    def forward(self, node_attr, edge_attr, edge_index, multi_data=None):
+        if multi_data is None:
+            raise ValueError("multi_data must be provided. Use MultiScaleGraphPreprocessor to preprocess graphs "
+                             "before training.")
+        require_device(node_attr, edge_attr, edge_index)
+        node_hidden = self.node_encoder(node_attr)
+        edge_hidden = self.edge_encoder(edge_attr)
+        eis = multi_data['edge_indices']
+        edge_attrs = [edge_hidden] + [torch.zeros(ei.shape[1], self.latent_dim, dtype=edge_hidden.dtype,
+                                                  device=edge_hidden.device) for ei in eis[1:]]
+        x = self.bsgmp(node_hidden, edge_attrs, eis, multi_data['node_indices'], multi_data['num_nodes'],
+                       multi_data['positions'])
+        return self.decoder(x)
+
+
+def create_bsms_model_from_config(config):
+    """bm@303: BSMS_MeshGraphNet from a config dict (the model block, or the dict itself)."""
+    mc = config.get('model', config) if isinstance(config, dict) else config
+    keys = ['input_node_dim', 'input_edge_dim', 'output_node_dim', 'num_levels', 'latent_dim', 'hidden_dim',
+            'pos_dim', 'num_hidden_layers_encoder', 'num_hidden_layers_decoder', 'activation_fn', 'dropout']
+    return BSMS_MeshGraphNet(**{k: mc[k] for k in keys if k in mc})

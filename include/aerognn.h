@@ -220,6 +220,74 @@ int agn_pool_edge_emit(int nc, const int32_t* cand_ptr, const int32_t* cand_sort
                        const int32_t* src, const int32_t* f2c, const int32_t* crowptr,
                        int32_t* csrc, int32_t* cdst, int32_t* cmem_ptr, int32_t* inv,
                        int64_t* crefkey, int e_fine, void* stream);
+/* ---------------------------------------------------------------------------------------
+ * BSMS-GNN bi-stride operators (stale models/bistride_ops + old models/bsms_mgn, recovered
+ * in SURVEY Appendix A; not reachable from the reference's train.py).
+ *   agn_bfs_distance     BistridePooling.bfs_distance (bistride_ops @21): hop distances over the
+ *                        out-adjacency (CSR rowptr/nbr of edge_index[0] -> [1]); -1 = unreachable.
+ *                        work: agn_bfs_work_ints(n) int32. Synchronises the stream per 32 levels.
+ *   agn_center_seed      argmin |pos - mean(pos)| (select_bistride_nodes @56, pos given)
+ *   agn_maxdeg_seed      argmax bincount(edge_index[0]) (pos absent); first index on ties
+ *   agn_bistride_select  where(dist even & >= 0), or where(dist >= 0) when that keeps < 30 %
+ *                        (ascending); *nsel returned on the host (synchronises)
+ *   agn_index_map        map[sel[j]] = j, -1 elsewhere (create_multiscale_graph @32)
+ *   agn_subgraph_edges   keep edges with both ends selected, remap, drop self loops (order kept)
+ *   agn_scatter_rows     out[idx[r]] = src[r] (Unpool.forward @102 after a zero fill)
+ *   agn_wec_forward/backward  WeightedEdgeConv (bistride_ops @131-210), see agn_wec_args
+ * ------------------------------------------------------------------------------------- */
+size_t agn_bfs_work_ints(int n);
+int agn_bfs_distance(const int32_t* rowptr, const int32_t* nbr, int n, int seed, int32_t* dist, int32_t* work,
+                     int* levels_out, void* stream);
+int agn_center_seed(const float* pos, int n, int pos_dim, int pos_ld, int32_t* seed, void* stream);
+int agn_maxdeg_seed(const int32_t* rowptr, int n, int32_t* seed, void* stream);
+size_t agn_compact_work_ints(int n);
+int agn_bistride_select(const int32_t* dist, int n, int32_t* sel, int* nsel, int32_t* work, void* stream);
+int agn_index_map(const int32_t* sel, int nsel, int n, int32_t* map, void* stream);
+int agn_subgraph_edges(const int64_t* src, const int64_t* dst, int e, const int32_t* map, int64_t* osrc,
+                       int64_t* odst, int* ecount, int32_t* work, void* stream);
+int agn_scatter_rows(int rows, int k, int dtype, const int32_t* idx, const void* src, int src_ld, void* out,
+                     int out_ld, void* stream);
+
+/* WeightedEdgeConv: w_e = sigmoid(w2 . relu(W1 [x_src, x_dst, |pos_dst - pos_src|] + b1) + b2),
+ * out_v = sum_{e: dst_e = v} (x T^T + b_T)[src_e] * w_e  ('mean': / max(deg_v, 1)).
+ * The node projections pab = [x W1a^T | x W1b^T + b1] and tx = x T^T + b_T come from
+ * agn_mlp_forward; edges are visited in the level's CSC order (sums in caller edge order). */
+typedef struct {
+  int n, e;
+  int dtype;                 /* AGN_F32 / AGN_BF16 (x, pab, tx, weights, out, grads) */
+  int out_dim;               /* 64 or 128 */
+  int hid;                   /* edge-weight MLP hidden width: 64 */
+  int pos_dim, pos_ld;       /* pos: fp32 [n][pos_ld], pos_dim <= 4 */
+  int mean;                  /* 0 = 'add', 1 = 'mean' */
+  const int32_t* rowptr;     /* CSC by receiver [n+1] */
+  const int32_t* src;        /* [e] CSC order */
+  const int32_t* dst;        /* [e] CSC order (backward) */
+  const int64_t* perm;       /* [e] CSC position -> caller edge id */
+  const int32_t* rowptr_src; /* CSR by sender [n+1] (backward) */
+  const int32_t* perm_src;   /* [e] CSR entries -> CSC positions (backward) */
+  const float* pos;
+  const void* pab;           /* [n][2*hid] */
+  const void* tx;            /* [n][out_dim] */
+  const float* w1c;          /* [hid] weight column of the edge length */
+  const float* w2;           /* [hid + 1] = second Linear's weight row | its bias b2 */
+  const void* w_in;          /* [e] given weights (caller order) or NULL = compute them */
+  void* w_out;               /* [e] computed weights (caller order) or NULL */
+  void* out;                 /* [n][out_dim]; NULL = weights only (compute_edge_weights) */
+  const void* dout;          /* backward: [n][out_dim] */
+  const void* gw;            /* backward: grad of the returned weights [e] (caller order) or NULL */
+  float* s_csc;              /* backward scratch: [e] weights in CSC order */
+  float* dh;                 /* backward scratch: [e][hid] */
+  void* dpa;                 /* backward out: [n][hid] */
+  void* dpb;                 /* backward out: [n][hid] */
+  void* dtx;                 /* backward out: [n][out_dim] */
+  void* dw_in;               /* backward out: grad of the given weights [e] (caller order) or NULL */
+  float* partial;            /* backward out: [agn_wec_blocks(n)][2*hid+1] = dw2 | dw1c | db2 partials */
+} agn_wec_args;
+
+int agn_wec_blocks(int n);
+int agn_wec_forward(const agn_wec_args* a, void* stream);
+int agn_wec_backward(const agn_wec_args* a, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,7 +33,10 @@ def test_struct_layouts_match_c(tmp_path):
               "agn_pack_desc": (L.PackDesc, ["src", "dst", "rows", "trans", "row_off", "dst_cols"]),
               "agn_mlp_fwd_args": (L.MlpFwdArgs, ["seg", "wpk", "bias", "ln_g", "proj", "resid", "act", "stats"]),
               "agn_mlp_bwd_args": (L.MlpBwdArgs, ["wtpk", "act", "g", "gidx", "gpre", "din_nseg", "din_k", "din",
-                                                 "din_resid", "ln_partial"])}
+                                                 "din_resid", "ln_partial"]),
+              "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db"]),
+              "agn_wgrad_batch": (L.WgradBatch, ["n", "d"]),
+              "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")])}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "aerognn.h"', 'int main(void){']
     for st, (_, fs) in fields.items():
         lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
