@@ -311,6 +311,29 @@ def cost_edge_bwd(E, N, H, s, nlin):
     return E * per + N * H * s, 2 * E * H * H * nlin
 
 
+def cost_edge_fwd_cat(E, N, H, s, nlin, train):
+    """Concat edge MLP (EdgeBlock / GMP): e and the two gathered node rows in, e' (+ saves) out."""
+    per = 4 * H * s + 8 + ((nlin - 1) * H * s + H * s + 8 if train else 0)
+    return E * per, 2 * E * H * (3 * H + (nlin - 1) * H)
+
+
+def cost_edge_bwd_cat(E, N, H, s, nlin):
+    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + 3 * H * s + 4
+    return E * per + N * H * s, 2 * E * H * (3 * H + (nlin - 1) * H)
+
+
+def cost_wec_fwd(E, N, out, s, hid=64):
+    """WeightedEdgeConv forward: per edge src/perm ids, P_a[src] and Tx[src] gathers, both
+    positions, the weight write; per receiver P_b, rowptr and the output row."""
+    return E * (12 + hid * s + out * s + 24 + s) + N * (8 + hid * s + out * s), E * (2 * hid + 2 * out + 16)
+
+
+def cost_wec_bwd(E, N, out, s, hid=64):
+    dst = E * (12 + out * s + hid * s + 24 + 4 + 4 * hid) + N * (out * s + 2 * hid * s)
+    src = E * (12 + out * s + 4 * hid) + N * (8 + out * s + hid * s)
+    return dst + src, E * (4 * hid + 4 * out)
+
+
 def cost_node_bwd(N, H, s, nlin):
     per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + 2 * H * s
     return N * per, 2 * N * H * (H * (nlin - 1) + 2 * H)

@@ -21,8 +21,9 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, bwd_nblocks, colsum_rows, cost_edge_bwd, cost_edge_fwd, cost_node_bwd,
-                   cost_node_fwd, cost_proj, dt_code, gather_rows, mlp_backward, mlp_forward, require_device,
+from .core import (Pack, WGrad, bwd_nblocks, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+                   cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
+                   timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_sum, stream)
 
 
@@ -334,7 +335,8 @@ class GMPFn(torch.autograd.Function):
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[ss, sd, se] if spec.gmp_order else [se, ss, sd],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), resid=e, out=e_out,
-                        acts=ea, hpre=ehp, stats=est)
+                        acts=ea, hpre=ehp, stats=est,
+                        tag="edge_fwd", cost=cost_edge_fwd_cat(E, N, H, x.element_size(), es.nlin, train))
         agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
         kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
         mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
@@ -387,8 +389,8 @@ class GMPFn(torch.autograd.Function):
                 [(H, de, True), (H, dxs, False), (H, dxd, False)]
         nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
-                     hpre=ehp, stats=est, din=din, ln_partial=part_e,
-                     tag="edge_bwd", cost=cost_edge_bwd(E, N, H, x.element_size(), es.nlin))
+                     hpre=ehp, stats=est, din=din, ln_partial=part_e, tag="edge_bwd",
+                     cost=(cost_edge_bwd if spec.trick else cost_edge_bwd_cat)(E, N, H, x.element_size(), es.nlin))
         g0 = gpre_e[0]
         grads_edge = []
         if spec.trick:
@@ -764,7 +766,8 @@ class WECFn(torch.autograd.Function):
         a.pos_dim, a.pos_ld, a.pos = pos32.shape[1], pos32.stride(0), ptr(pos32)
         a.pab, a.tx, a.w1c, a.w2 = ptr(pab), ptr(tx), spec.pack["w1c"], spec.pack["w2"]
         a.w_out, a.out = ptr(w), ptr(out)
-        check(L.lib().agn_wec_forward(C.byref(a), stream()), "wec_forward")
+        with timed("wec_fwd", cost_wec_fwd(E, N, spec.out, x.element_size())):
+            check(L.lib().agn_wec_forward(C.byref(a), stream()), "wec_forward")
         ctx.spec, ctx.level, ctx.mean = spec, level, mean
         ctx.save_for_backward(x, pos32, pab, tx)
         ctx.set_materialize_grads(False)
@@ -792,7 +795,8 @@ class WECFn(torch.autograd.Function):
         dw = _c(dw) if dw is not None else None
         a.dout, a.gw = ptr(dout), ptr(dw)
         a.s_csc, a.dh, a.dpa, a.dpb, a.dtx, a.partial = ptr(s_csc), ptr(dh), ptr(dpa), ptr(dpb), ptr(dtx), ptr(partial)
-        check(L.lib().agn_wec_backward(C.byref(a), stream()), "wec_backward")
+        with timed("wec_bwd", cost_wec_bwd(E, N, spec.out, x.element_size())):
+            check(L.lib().agn_wec_backward(C.byref(a), stream()), "wec_backward")
         i, o = spec.inp, spec.out
         dx = torch.empty_like(x)
         mlp_forward(rows=N, dtype=dt, hidden=i, nlin=1, out_dim=i,
