@@ -35,7 +35,7 @@ class MlpFwdArgs(C.Structure):
                 ("ln_g", vp), ("ln_b", vp),
                 ("proj", vp), ("src", vp), ("dst", vp),
                 ("resid", vp), ("out", vp),
-                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp)]
+                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32)]
 
 
 class MlpBwdArgs(C.Structure):
@@ -47,7 +47,7 @@ class MlpBwdArgs(C.Structure):
                 ("gpre", vp * MAX_LIN),
                 ("din_nseg", i32), ("din_k", i32 * MAX_SEG),
                 ("din", vp * MAX_SEG), ("din_resid", i32 * MAX_SEG),
-                ("ln_partial", vp)]
+                ("ln_partial", vp), ("tiled", i32), ("gpre_tiled", i32)]
 
 
 MAX_WGRAD = 8
@@ -55,7 +55,8 @@ MAX_WGRAD = 8
 
 class WgradDesc(C.Structure):
     _fields_ = [("g", vp), ("x", vp), ("ldg", i32), ("ldx", i32), ("m", i32), ("k", i32), ("rows", i32),
-                ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp)]
+                ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp),
+                ("g_tiled", i32), ("x_tiled", i32)]
 
 
 class WgradBatch(C.Structure):

@@ -54,6 +54,23 @@ def dt_code(dtype) -> int:
     raise NotImplementedError(f"aerognn kernels compute in float32 or bfloat16, got {dtype}")
 
 
+def tiled_empty(rows, width, dtype, device):
+    """[rows, width] buffer in the AGN_TILED layout (aerognn.h): rows padded to 32, only
+    libaerognn reads it. Tagged so mlp_forward / mlp_backward / WGrad pass the layout on."""
+    t = torch.empty((rows + 31) // 32 * 32, width, dtype=dtype, device=device)
+    t.agn_tiled = True
+    t.agn_rows = rows
+    return t
+
+
+def is_tiled(t) -> bool:
+    return t is not None and getattr(t, "agn_tiled", False)
+
+
+def logical_rows(t) -> int:
+    return getattr(t, "agn_rows", t.shape[0])
+
+
 def require_device(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -175,6 +192,7 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
         for i, t in enumerate(acts):
             a.act[i] = ptr(t)
     a.hpre, a.stats = ptr(hpre), ptr(stats)
+    a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
     with timed(tag, cost):
         check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
 
@@ -198,6 +216,8 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
         a.act[i] = ptr(t)
     a.hpre, a.stats, a.ln_g = ptr(hpre), ptr(stats), ln_g
     a.g, a.g2, a.gidx = ptr(g), ptr(g2), ptr(gidx)
+    a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
+    a.gpre_tiled = sum(1 << l for l in range(nlin) if is_tiled(gpre[l]))
     a.din_nseg = len(din)
     for i, (k, t, r) in enumerate(din):
         a.din_k[i] = k
@@ -253,7 +273,7 @@ class WGrad:
         self.items = []
 
     def add(self, G, X, dw, db=None):
-        assert G.dtype == X.dtype and G.shape[0] == X.shape[0]
+        assert G.dtype == X.dtype and logical_rows(G) == logical_rows(X)
         assert dw.dtype == torch.float32 and dw.stride(1) == 1
         self.items.append((G, X, dw, db))
 
@@ -261,7 +281,7 @@ class WGrad:
         lib = L.lib()
         for i in range(0, len(self.items), L.MAX_WGRAD):
             chunk = self.items[i:i + L.MAX_WGRAD]
-            rows = max(it[0].shape[0] for it in chunk)
+            rows = max(logical_rows(it[0]) for it in chunk)
             dev = chunk[0][0].device
             if rows == 0:
                 for G, X, dw, db in chunk:
@@ -284,8 +304,9 @@ class WGrad:
                 if db is not None:
                     dbp = scratch[o:o + bsz[j]]
                     o += bsz[j]
-                b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], G.shape[0],
-                                     dw.stride(0), ptr(dwp), ptr(dbp), ptr(dw), ptr(db))
+                b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], logical_rows(G),
+                                     dw.stride(0), ptr(dwp), ptr(dbp), ptr(dw), ptr(db), int(is_tiled(G)),
+                                     int(is_tiled(X)))
             check(lib.agn_wgrad(C.byref(b), dt_code(chunk[0][0].dtype), ns, stream()), "wgrad")
         self.items = []
 

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, bwd_nblocks, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+from .core import (Pack, WGrad, bwd_nblocks, tiled_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_sum, stream)
@@ -52,6 +52,9 @@ class ChainSpec:
         self.nlin = len(linears)
         self.in_dim = linears[0][0].shape[1]
         self.out_dim = linears[-1][0].shape[0]
+        # training saves (ReLU outputs, pre-LN output) go to the AGN_TILED layout when hidden-wide
+        # (agn_wgrad reads tiled operands of width 128 = the production hidden size)
+        self.tiled_saves = hidden == 128 and (ln is None or self.out_dim == hidden)
         self.p = prefix
         for l, (w, b) in enumerate(linears):
             M, K = w.shape
@@ -99,12 +102,26 @@ class ChainSpec:
 def _alloc_saves(spec, rows, dtype, dev, train):
     if not train:
         return None, None, None
-    acts = [torch.empty(rows, spec.hidden, dtype=dtype, device=dev) for _ in range(spec.nlin - 1)]
+    emp = tiled_empty if spec.tiled_saves else (lambda r, w, dt, d: torch.empty(r, w, dtype=dt, device=d))
+    acts = [emp(rows, spec.hidden, dtype, dev) for _ in range(spec.nlin - 1)]
     hpre = stats = None
     if spec.ln is not None:
-        hpre = torch.empty(rows, spec.out_dim, dtype=dtype, device=dev)
+        hpre = emp(rows, spec.out_dim, dtype, dev)
         stats = torch.empty(rows, 2, dtype=torch.float32, device=dev)
     return acts, hpre, stats
+
+
+def _alloc_gpre(spec, rows, dtype, dev, rowmajor=()):
+    """Pre-activation gradient buffers: AGN_TILED when hidden-wide (read only by agn_wgrad), row
+    major for layers listed in `rowmajor` (consumed by other kernels) or narrower than hidden."""
+    out = []
+    for l in range(spec.nlin):
+        w = spec.hidden if l < spec.nlin - 1 else spec.out_dim
+        if w == spec.hidden == 128 and l not in rowmajor:
+            out.append(tiled_empty(rows, w, dtype, dev))
+        else:
+            out.append(torch.empty(rows, w, dtype=dtype, device=dev))
+    return out
 
 
 def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk, wg=None):
@@ -181,8 +198,7 @@ class MLPFn(torch.autograd.Function):
         gy = _c(gy)
         rows = x.shape[0]
         dt = x.dtype
-        gpre = [torch.empty(rows, spec.hidden if l < spec.nlin - 1 else spec.out_dim, dtype=dt, device=x.device)
-                for l in range(spec.nlin)]
+        gpre = _alloc_gpre(spec, rows, dt, x.device)
         ks = _ksegs(x, spec.hidden)
         dparts = [torch.empty(rows, k, dtype=dt, device=x.device) if ctx.needs_input_grad[0] else None
                   for _, k in ks]
@@ -364,7 +380,7 @@ class GMPFn(torch.autograd.Function):
         gx = _c(gx) if gx is not None else torch.zeros_like(x)
         ge = _c(ge) if ge is not None else None
         # ---- NodeBlock: d(x), d(agg)
-        gpre_n = [torch.empty(N, H, dtype=dt, device=dev) for _ in range(ns.nlin)]
+        gpre_n = _alloc_gpre(ns, N, dt, dev)
         dx = torch.empty_like(x)
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb_n = bwd_nblocks(N)
@@ -376,7 +392,7 @@ class GMPFn(torch.autograd.Function):
         if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
             dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
         # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
-        gpre_e = [torch.empty(E, H, dtype=dt, device=dev) for _ in range(es.nlin)]
+        gpre_e = _alloc_gpre(es, E, dt, dev, rowmajor=(0,) if spec.trick else ())  # trick: dP_s/dP_d sums read g0
         nb_e = bwd_nblocks(E)
         part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
         de = torch.empty_like(e)
@@ -572,7 +588,7 @@ class EdgeBlockFn(torch.autograd.Function):
         dt, dev = x.dtype, x.device
         N, E, H = x.shape[0], e.shape[0], spec.H
         g = _c(g)
-        gpre = [torch.empty(E, H, dtype=dt, device=dev) for _ in range(es.nlin)]
+        gpre = _alloc_gpre(es, E, dt, dev, rowmajor=(0,) if spec.trick else ())
         nb = bwd_nblocks(E)
         part = torch.empty(nb, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
         de = torch.empty_like(e)
@@ -644,7 +660,7 @@ class NodeBlockFn(torch.autograd.Function):
         dt, dev = x.dtype, x.device
         N, E, H = x.shape[0], e.shape[0], spec.H
         g = _c(g)
-        gpre = [torch.empty(N, H, dtype=dt, device=dev) for _ in range(ns.nlin)]
+        gpre = _alloc_gpre(ns, N, dt, dev)
         dx = torch.empty_like(x)
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb = bwd_nblocks(N)

@@ -141,6 +141,90 @@ AGN_DEV void store_row_w(T* rowp, const float (&v)[NR], int h, bool valid) {
   }
 }
 
+// ---------------------------------------------------------------- AGN_TILED saves (aerognn.h)
+// 16-B unit index of (row, unit i of the lane's NR registers, half h); U = units per lane-row.
+template <typename T, int NR>
+AGN_DEV size_t tiled_unit(int row, int i, int h) {
+  constexpr int U = NR * (int)sizeof(T) / 16;
+  return ((size_t)(row >> 5) * U + i) * 64 + (row & 31) + 32 * h;
+}
+template <typename T, int NR>
+AGN_DEV void store_row_tiled(T* base, const float (&v)[NR], int row, int h, bool valid) {
+  if (!valid) return;
+  uint4* b = reinterpret_cast<uint4*>(base);
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+      b[tiled_unit<T, NR>(row, i, h)] = __builtin_bit_cast(
+          uint4, u32x4{pack2(v[8 * i], v[8 * i + 1]), pack2(v[8 * i + 2], v[8 * i + 3]),
+                       pack2(v[8 * i + 4], v[8 * i + 5]), pack2(v[8 * i + 6], v[8 * i + 7])});
+  } else {
+#pragma unroll
+    for (int i = 0; i < NR / 4; ++i)
+      b[tiled_unit<T, NR>(row, i, h)] = __builtin_bit_cast(uint4, f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]});
+  }
+}
+template <typename T, int NR>
+AGN_DEV void load_row_tiled(float (&v)[NR], const T* base, int row, int h) {
+  const uint4* b = reinterpret_cast<const uint4*>(base);
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      const u32x4 x = __builtin_bit_cast(u32x4, b[tiled_unit<T, NR>(row, i, h)]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[8 * i + 2 * j] = lo_bf16(x[j]); v[8 * i + 2 * j + 1] = hi_bf16(x[j]); }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NR / 4; ++i) {
+      const f32x4 x = __builtin_bit_cast(f32x4, b[tiled_unit<T, NR>(row, i, h)]);
+      v[4 * i] = x[0]; v[4 * i + 1] = x[1]; v[4 * i + 2] = x[2]; v[4 * i + 3] = x[3];
+    }
+  }
+}
+// register quad q (features 8q+4h..+3) of a tiled row
+template <typename T, int NR>
+AGN_DEV f32x4 load4_tiled(const T* base, int q, int row, int h) {
+  if constexpr (sizeof(T) == 2) {
+    const bf16* p = base + tiled_unit<T, NR>(row, q >> 1, h) * 8 + 4 * (q & 1);
+    return load4(p);
+  } else {
+    return load4(base + tiled_unit<T, NR>(row, q, h) * 4);
+  }
+}
+template <typename T, int NR>
+AGN_DEV void store4_tiled(T* base, int q, int row, int h, f32x4 v) {
+  if constexpr (sizeof(T) == 2) store4(base + tiled_unit<T, NR>(row, q >> 1, h) * 8 + 4 * (q & 1), v);
+  else store4(base + tiled_unit<T, NR>(row, q, h) * 4, v);
+}
+// unit i of a pair loop (8 registers 8i..8i+7): bf16 = one unit, fp32 = units 2i, 2i+1
+template <typename T, int NR>
+AGN_DEV void store8_tiled(T* base, int i, int row, int h, const float (&v)[8], bool valid) {
+  if (!valid) return;
+  uint4* b = reinterpret_cast<uint4*>(base);
+  if constexpr (sizeof(T) == 2) {
+    b[tiled_unit<T, NR>(row, i, h)] =
+        __builtin_bit_cast(uint4, u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])});
+  } else {
+    b[tiled_unit<T, NR>(row, 2 * i, h)] = __builtin_bit_cast(uint4, f32x4{v[0], v[1], v[2], v[3]});
+    b[tiled_unit<T, NR>(row, 2 * i + 1, h)] = __builtin_bit_cast(uint4, f32x4{v[4], v[5], v[6], v[7]});
+  }
+}
+template <typename T, int NR>
+AGN_DEV void load8_tiled(float (&v)[8], const T* base, int i, int row, int h) {
+  const uint4* b = reinterpret_cast<const uint4*>(base);
+  if constexpr (sizeof(T) == 2) {
+    const u32x4 x = __builtin_bit_cast(u32x4, b[tiled_unit<T, NR>(row, i, h)]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf16(x[j]); v[2 * j + 1] = hi_bf16(x[j]); }
+  } else {
+    const f32x4 x = __builtin_bit_cast(f32x4, b[tiled_unit<T, NR>(row, 2 * i, h)]);
+    const f32x4 y = __builtin_bit_cast(f32x4, b[tiled_unit<T, NR>(row, 2 * i + 1, h)]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = x[j]; v[4 + j] = y[j]; }
+  }
+}
+
 // Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
 // rows) above the MFMA chain, where they would sit live in registers across every layer.
 AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
@@ -207,6 +291,13 @@ template <int NR> struct BOp<bf16, NR> {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (float)u[i][j];
   }
+  // AGN_TILED store: the packed registers as they are (no lane exchange)
+  AGN_DEV void store_tiled(bf16* base, int row, int h, bool valid) const {
+    if (!valid) return;
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+      reinterpret_cast<uint4*>(base)[tiled_unit<bf16, NR>(row, i, h)] = __builtin_bit_cast(uint4, u[i]);
+  }
   // store the packed activations as a row of `H` bf16, 16 B per lane (see store8_w)
   AGN_DEV void store(bf16* rowp, int h, bool valid) const {
 #pragma unroll
@@ -239,6 +330,9 @@ template <int NR> struct BOp<float, NR> {
   AGN_DEV void get8(float (&o)[8], int i) const {
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = u[8 * i + j];
+  }
+  AGN_DEV void store_tiled(float* base, int row, int h, bool valid) const {
+    store_row_tiled<float, NR>(base, u, row, h, valid);
   }
   AGN_DEV void store(float* rowp, int h, bool valid) const {
     if (!valid) return;

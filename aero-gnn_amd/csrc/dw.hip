@@ -39,7 +39,31 @@ struct StageRegs {
   static constexpr int NCH = DW_ROWS * CHUNKS / DW_THREADS;     // chunks per thread
   uint4 v[NCH];
 
-  AGN_DEV void load(const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0) {
+  // AGN_TILED operand (aerognn.h): a 64-row stage of a 128-wide tiled matrix is 64*CHUNKS
+  // consecutive 16-B units (r0 is a multiple of 64), so the loads are contiguous.
+  static AGN_DEV void tiled_pos(int u, int& row, int& i, int& hh) {
+    const int t = u / (CHUNKS * 32), rem = u - t * (CHUNKS * 32);
+    i = rem >> 6;
+    row = t * 32 + (rem & 31);
+    hh = (rem >> 5) & 1;
+  }
+  AGN_DEV void load(const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0, int tiled) {
+    if (tiled) {
+      const uint4* gu = reinterpret_cast<const uint4*>(g) + (size_t)(r0 >> 5) * (CHUNKS / 2) * 64;
+      if (r0 + DW_ROWS <= rows) {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) v[j] = gu[threadIdx.x + j * DW_THREADS];
+      } else {
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+          const int u = threadIdx.x + j * DW_THREADS;
+          int row, i, hh;
+          tiled_pos(u, row, i, hh);
+          v[j] = (r0 + row < rows) ? gu[u] : uint4{0u, 0u, 0u, 0u};
+        }
+      }
+      return;
+    }
     const bool fast = ((ld % PER16) == 0) && ((c0 % PER16) == 0) && (cols - c0 >= DW_BLK) && (r0 + DW_ROWS <= rows);
     if (fast) {
 #pragma unroll
@@ -64,8 +88,24 @@ struct StageRegs {
       }
     }
   }
-  AGN_DEV void store(T* lds) const {
+  AGN_DEV void store(T* lds, int tiled) const {
     constexpr int LD = DwTile<T>::LD;
+    if (tiled) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        int row, i, hh;
+        tiled_pos(threadIdx.x + j * DW_THREADS, row, i, hh);
+        if constexpr (sizeof(T) == 2) {  // features 16i+4hh+{0..3} | 16i+8+4hh+{0..3}
+          const u32x4 x = __builtin_bit_cast(u32x4, v[j]);
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2*>(lds + row * LD + 16 * i + 4 * hh) = u32x2{x[0], x[1]};
+          *reinterpret_cast<u32x2*>(lds + row * LD + 16 * i + 8 + 4 * hh) = u32x2{x[2], x[3]};
+        } else {  // features 8i+4hh+{0..3}
+          *reinterpret_cast<uint4*>(lds + row * LD + 8 * i + 4 * hh) = v[j];
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
       const int i = threadIdx.x + j * DW_THREADS;
@@ -118,17 +158,17 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   float bsum = 0.f;  // bias colsum partial (threads 0..127 own columns m0 + tid)
   StageRegs<T> rg, rx;
   if (rbeg < rend) {
-    rg.load(G, d.ldg, rend, d.m, rbeg, m0);
-    rx.load(X, d.ldx, rend, d.k, rbeg, k0);
+    rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
+    rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled);
   }
   for (int r0 = rbeg; r0 < rend; r0 += DW_ROWS) {
     __syncthreads();
-    rg.store(sg);
-    rx.store(sx);
+    rg.store(sg, d.g_tiled);
+    rx.store(sx, d.x_tiled);
     __syncthreads();
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
-      rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0);
-      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0);
+      rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
+      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled);
     }
     if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK) {
 #pragma unroll 8
@@ -294,6 +334,7 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   for (int i = 0; i < b->n; ++i) {
     const agn_wgrad_desc& d = b->d[i];
     if (d.m < 1 || d.k < 1 || d.rows < 0) return AGN_E_ARG;
+    if ((d.g_tiled && d.m != DW_BLK) || (d.x_tiled && d.k != DW_BLK)) return AGN_E_SHAPE;
     const int nb = ((d.m + DW_BLK - 1) / DW_BLK) * ((d.k + DW_BLK - 1) / DW_BLK);
     maxblk = nb > maxblk ? nb : maxblk;
   }

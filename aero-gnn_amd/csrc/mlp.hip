@@ -235,7 +235,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       __syncthreads();
       stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
       b.template set_relu<NT>(acc);
-      if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
+      if (a.act[l - 1]) {
+        if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
+        else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
+      }
       if (OUT_FULL || !last) acc_bias<NT, true>(acc, a.bias[l], H, h);
       else acc_bias<NT, false>(acc, a.bias[l], outl, h);
       __syncthreads();
@@ -274,7 +277,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
 #pragma unroll
         for (int e = 0; e < 8; ++e) v8[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
         if (a.use_ln) {
-          if (hp) store8_w(hp, i, h, v8, valid);
+          if (hp) {
+            if (a.tiled) store8_tiled<T, NR>(reinterpret_cast<T*>(a.hpre), i, row, h, v8, valid);
+            else store8_w(hp, i, h, v8, valid);
+          }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const int f0 = 16 * i + 8 * j + 4 * h;
@@ -301,7 +307,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         f32x4 v = {acc[q / 4][4 * (q % 4)], acc[q / 4][4 * (q % 4) + 1], acc[q / 4][4 * (q % 4) + 2],
                    acc[q / 4][4 * (q % 4) + 3]};
         if (MODE != M_NOUT && a.use_ln) {
-          if (hp && valid) store4_masked(hp, f0, outd, false, v);
+          if (hp && valid) {
+            if (a.tiled) store4_tiled<T, NR>(reinterpret_cast<T*>(a.hpre), q, row, h, v);  // outd == H
+            else store4_masked(hp, f0, outd, false, v);
+          }
           f32x4 g4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -380,7 +389,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
 #pragma unroll
     for (int q = 0; q < NR / 4; ++q) {
       const int f0 = 8 * q + 4 * h;
-      const f32x4 hv = VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
+      const f32x4 hv = a.tiled ? load4_tiled<T, NR>(reinterpret_cast<const T*>(a.hpre), q, rr, h)  // M == H
+                       : VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
       f32x4 gm = {0.f, 0.f, 0.f, 0.f};
       if (VEC) gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
       else {
@@ -420,7 +430,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
 #pragma unroll
     for (int q = 0; q < NR / 4; ++q) {
       const int f0 = 8 * q + 4 * h;
-      const f32x4 hv = VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
+      const f32x4 hv = a.tiled ? load4_tiled<T, NR>(reinterpret_cast<const T*>(a.hpre), q, rr, h)  // M == H
+                       : VEC ? load4(hp + f0) : load4_masked(hp, f0, M, false);
       f32x4 gm = {0.f, 0.f, 0.f, 0.f};
       if (VEC) gm = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
       else {
@@ -442,7 +453,9 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
   for (int l = a.nlin - 1; l >= 0; --l) {
     const int Ml = (l == a.nlin - 1) ? M : H;
     const int kuM = units_k<T>(Ml);
-    if (a.gpre[l]) {
+    if (a.gpre[l] && ((a.gpre_tiled >> l) & 1)) {
+      store_row_tiled<T, NR>(reinterpret_cast<T*>(a.gpre[l]), A, row, h, valid);
+    } else if (a.gpre[l]) {
       T* gp = reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * Ml;
       if (VEC || (MODE == M_NOUT && l < a.nlin - 1)) store_row<T, NR, true>(gp, Ml, A, h, valid);
       else store_row<T, NR, false>(gp, Ml, A, h, valid);
@@ -457,7 +470,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       gemm<T, NT, NR, true>(acc, b, kuM, wl, kuM, NT, lane);
       float m[NR];
       cbarrier();
-      load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
+      if (a.tiled) load_row_tiled<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]), rr, h);
+      else load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
       acc_to_regs<NT, NR>(A, acc);
 #pragma unroll
       for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? A[i] : 0.f;
@@ -585,7 +599,10 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
-      if (a.act[l - 1]) b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
+      if (a.act[l - 1]) {
+        if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
+        else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
+      }
       acc_bias_lds<NT>(acc, pv[l], h);
       gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
     }
@@ -619,7 +636,10 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
       if (a.use_ln) {
-        if (hp) store8_w(hp, i, h, v, valid);
+        if (hp) {
+          if (a.tiled) store8_tiled<T, NR>(reinterpret_cast<T*>(a.hpre), i, row, h, v, valid);
+          else store8_w(hp, i, h, v, valid);
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int f0 = 16 * i + 8 * j + 4 * h;
@@ -712,7 +732,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float hv[8];
-        load8_w(hv, hp, i, h);
+        if (a.tiled) load8_tiled<T, NR>(hv, reinterpret_cast<const T*>(a.hpre), i, rr, h);
+        else load8_w(hv, hp, i, h);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
@@ -744,7 +765,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float hv[8];
-        load8_w(hv, hp, i, h);
+        if (a.tiled) load8_tiled<T, NR>(hv, reinterpret_cast<const T*>(a.hpre), i, rr, h);
+        else load8_w(hv, hp, i, h);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
@@ -761,14 +783,18 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
     BOp<T, NR> b;
     for (int l = a.nlin - 1; l >= 0; --l) {
       cbarrier();
-      if (a.gpre[l]) store_row_w<T, NR>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, A, h, valid);
+      if (a.gpre[l]) {
+        if ((a.gpre_tiled >> l) & 1) store_row_tiled<T, NR>(reinterpret_cast<T*>(a.gpre[l]), A, row, h, valid);
+        else store_row_w<T, NR>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, A, h, valid);
+      }
       b.set(A);
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
       if (l > 0) {
         gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
         float m[NR];
-        load_row_w<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, h);
+        if (a.tiled) load_row_tiled<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]), rr, h);
+        else load_row_w<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, h);
 #pragma unroll
         for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? acc[i / 16][i % 16] : 0.f;
       } else if (a.din[0]) {

@@ -78,6 +78,8 @@ typedef struct {
   void* act[AGN_MAX_LIN];          /* relu output of layer l (l < nlin-1), [rows][hidden], 16-B aligned */
   void* hpre;                      /* last Linear output before LN, [rows][out_dim] */
   float* stats;                    /* [rows][2] = mean, rstd */
+  int tiled;                       /* 1: act/hpre in the tiled layout (AGN_TILED below, hidden-wide) */
+  int _pad2;
 } agn_mlp_fwd_args;
 
 typedef struct {
@@ -106,7 +108,16 @@ typedef struct {
   void* din[AGN_MAX_SEG];          /* NULL = not needed */
   int din_resid[AGN_MAX_SEG];      /* 1: din[s] = g(+g2) + W0^T dh0 (residual of the block) */
   float* ln_partial;               /* [agn_mlp_bwd_nwaves(rows)][2][out_dim]: sum g*xhat, sum g */
+  int tiled;                       /* 1: act/hpre are read in the tiled layout */
+  int gpre_tiled;                  /* bit l: gpre[l] written in the tiled layout (hidden-wide only) */
 } agn_mlp_bwd_args;
+
+/* AGN_TILED layout of a [rows][H] activation saved for the backward (H = hidden, rows padded to
+ * a multiple of 32): the 16-B register units of the 32-row wave that produced it, in register
+ * order. Unit (row r, i, half h) lives at 16-B index ((r / 32) * U + i) * 64 + (r % 32) + 32 h,
+ * U = H * elem_size / 16; for bf16 it holds features 16i+4h+{0..3} and 16i+8+4h+{0..3}, for fp32
+ * features 8i+4h+{0..3}. One wave store/load instruction moves 1 KB contiguous. Only libaerognn
+ * kernels read it (the MLP backward and agn_wgrad). */
 
 /* Pack an A operand A[r][k] = trans ? W[k][r] : W[r][k] (r < rows, k < cols) into rows
  * [row_off, row_off+rows) x cols [col_off, col_off+cols) of a packed [dst_rows x dst_cols]
@@ -141,6 +152,7 @@ typedef struct {
   float* db_partial;    /* nsplit * round_up(m, 128) scratch, or NULL (no bias) */
   float* dw;            /* [m][ldw] fp32 output */
   float* db;            /* [m] fp32 output or NULL */
+  int g_tiled, x_tiled; /* operand in the AGN_TILED layout (then m resp. k == 128) */
 } agn_wgrad_desc;
 typedef struct {
   int n;
