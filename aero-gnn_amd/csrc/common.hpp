@@ -182,6 +182,11 @@ AGN_DEV void load_row_tiled(float (&v)[NR], const T* base, int row, int h) {
     }
   }
 }
+AGN_DEV void unpack8(float (&v)[8], uint4 u) {
+  const u32x4 x = __builtin_bit_cast(u32x4, u);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf16(x[j]); v[2 * j + 1] = hi_bf16(x[j]); }
+}
 // register quad q (features 8q+4h..+3) of a tiled row
 template <typename T, int NR>
 AGN_DEV f32x4 load4_tiled(const T* base, int q, int row, int h) {

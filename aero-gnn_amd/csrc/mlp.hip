@@ -698,6 +698,7 @@ AGN_DEV void add_grad_w(float (&v)[NR], const agn_mlp_bwd_args& a, int rr, int h
 
 template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp_bwd_args a) {
+  static_assert(sizeof(T) == 2, "resident kernels are bf16-only");
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NP = (NR >= 32) ? NR / 32 : 1;
@@ -729,11 +730,23 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
       const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * H;
       float B[NR];
       float c1 = 0.f, c2 = 0.f;
+      // the pre-LN row is read once and kept packed (32 VGPRs) for both LN passes
+      uint4 hraw[NR / 8];
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        if (a.tiled) {
+          hraw[i] = reinterpret_cast<const uint4*>(a.hpre)[tiled_unit<T, NR>(rr, i, h)];
+        } else {
+          float t8[8];
+          load8_w(t8, hp, i, h);
+          hraw[i] = __builtin_bit_cast(uint4, u32x4{pack2(t8[0], t8[1]), pack2(t8[2], t8[3]), pack2(t8[4], t8[5]),
+                                                    pack2(t8[6], t8[7])});
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float hv[8];
-        if (a.tiled) load8_tiled<T, NR>(hv, reinterpret_cast<const T*>(a.hpre), i, rr, h);
-        else load8_w(hv, hp, i, h);
+        unpack8(hv, hraw[i]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
@@ -765,8 +778,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float hv[8];
-        if (a.tiled) load8_tiled<T, NR>(hv, reinterpret_cast<const T*>(a.hpre), i, rr, h);
-        else load8_w(hv, hp, i, h);
+        unpack8(hv, hraw[i]);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const f32x4 gm = *reinterpret_cast<const f32x4*>(pg_lds + 16 * i + 8 * j + 4 * h);
