@@ -99,6 +99,74 @@ AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
 #pragma unroll
   for (int e = 0; e < 4; ++e) { o[e] = x[e]; o[4 + e] = y[e]; }
 }
+// ---------------------------------------------------------------- LDS-staged coalesced tile I/O
+// A wave's 32-row tile of a row-major [rows][H] bf16 matrix (H = 8 * NC chunks of 16 B) moves
+// through an 8-row LDS staging area `stg` (8 x NC uint4, private to the wave) in 4 passes, so
+// every global access instruction covers 1 KB contiguous. In registers each lane keeps the
+// row's chunks in "exchanged" form: chunk 2i + h of row c (what pack8_w produces).
+template <int NC>
+AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane) {
+  constexpr int PER = 64 / NC;  // rows covered by one 1-KB instruction
+  const int c = lane & 31, h = lane >> 5;
+  uint4 raw[32 / PER];
+#pragma unroll
+  for (int k = 0; k < 32 / PER; ++k) {
+    const int q = lane + 64 * k;
+    raw[k] = (q / NC < nvalid) ? reinterpret_cast<const uint4*>(tile_base)[q] : uint4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+#pragma unroll
+    for (int k = 0; k < 8 / PER; ++k) {
+      const int q = lane + 64 * k;  // chunk within the 8-row block
+      stg[q / NC][q % NC] = raw[p * (8 / PER) + k];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < NC / 2; ++i) {
+      const uint4 v = stg[c & 7][2 * i + h];
+      if ((c >> 3) == p) mine[i] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+template <int NC>
+AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane) {
+  constexpr int PER = 64 / NC;
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    if ((c >> 3) == p) {
+#pragma unroll
+      for (int i = 0; i < NC / 2; ++i) stg[c & 7][2 * i + h] = mine[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int k = 0; k < 8 / PER; ++k) {
+      const int q = lane + 64 * k;
+      const uint4 v = stg[q / NC][q % NC];
+      if (8 * p + q / NC < nvalid) reinterpret_cast<uint4*>(tile_base)[(8 * p) * NC + q] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+// exchanged chunk -> acc-layout floats (the lane-half exchange of load8_w)
+AGN_DEV void unpack8_w(float (&o)[8], uint4 u) {
+  const u32x4 x = __builtin_bit_cast(u32x4, u);
+  uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  o[0] = lo_bf16(a0); o[1] = hi_bf16(a0); o[2] = lo_bf16(a1); o[3] = hi_bf16(a1);
+  o[4] = lo_bf16(b0); o[5] = hi_bf16(b0); o[6] = lo_bf16(b1); o[7] = hi_bf16(b1);
+}
+
+// pack + lane-half exchange of store8_w without the store: chunk (2i + h) of the row
+AGN_DEV uint4 pack8_w(const float (&v)[8], int h) {
+  uint32_t a0 = pack2(v[0], v[1]), a1 = pack2(v[2], v[3]), b0 = pack2(v[4], v[5]), b1 = pack2(v[6], v[7]);
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  return __builtin_bit_cast(uint4, u32x4{a0, a1, b0, b1});
+}
 AGN_DEV void store8_w(bf16* rowp, int i, int h, const float (&v)[8], bool valid) {
   uint32_t a0 = pack2(v[0], v[1]), a1 = pack2(v[2], v[3]), b0 = pack2(v[4], v[5]), b1 = pack2(v[6], v[7]);
   swap_halves(a0, b0);

@@ -524,6 +524,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
 constexpr int RES_WPB = 8;
 constexpr int RES_BLOCK = 64 * RES_WPB;
 constexpr int RES_MAXL = 4;
+// LDS-staged g loads / de stores in the resident backward: coalesced, but at 256 VGPRs the extra
+// live registers spill (measured: 2.55 -> 2.88 ms per launch with de staging), so both stay off
+constexpr bool kStageGradIn = false;
+constexpr bool kStageGradOut = false;
 
 template <typename T, int NT>
 constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
@@ -556,6 +560,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
+  __shared__ uint4 stg[RES_WPB][8][H / 8];  // per-wave 8-row staging: coalesced e' stores
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
@@ -588,7 +593,20 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     }
     {
       float v[NR];
-      load_row_w<T, NR>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
+      if (sg.ld == H) {  // coalesced 1-KB loads through the wave's LDS staging rows
+        uint4 mine[NR / 8];
+        tile_load_chunks<H / 8>(mine, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                                stg[threadIdx.x >> 6], lane);
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) {
+          float o[8];
+          unpack8_w(o, mine[i]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
+        }
+      } else {
+        load_row_w<T, NR>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
+      }
       b.set(v);
     }
     // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
@@ -630,6 +648,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * H : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
+    const bool stage_out = a.out_ld == H;
+    uint4 ob[NR / 8];  // e' row as 16-B chunks (chunk 2i+h of the row), for the staged store
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
       float v[8];
@@ -656,8 +676,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = round_t<T>(v[e]) + r[e];
       }
-      store8_w(op, i, h, v, valid);
+      if (stage_out) ob[i] = pack8_w(v, h);
+      else store8_w(op, i, h, v, valid);
     }
+    if (stage_out)  // 8-row passes through LDS: every store instruction writes 1 KB contiguous
+      tile_store_chunks<H / 8>(ob, reinterpret_cast<T*>(a.out) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                               stg[threadIdx.x >> 6], lane);
   }
 }
 
@@ -707,6 +731,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ float lnp[RES_WPB][2][H];
   __shared__ __attribute__((aligned(16))) float pg_lds[H];  // LN gamma
+  __shared__ uint4 stg[RES_WPB][8][H / 8];  // per-wave 8-row staging: coalesced g / de
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
   for (int i = threadIdx.x; i < H; i += RES_BLOCK) pg_lds[i] = a.use_ln ? a.ln_g[i] : 0.f;
   __syncthreads();
@@ -724,7 +749,26 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
     float A[NR];
-    load_grad_w<T, NR>(A, a, rr, valid, h);
+    if (kStageGradIn && a.g && a.out_dim == H) {  // incoming gradient: coalesced 1-KB loads through LDS
+      uint4 mine[NR / 8];
+      tile_load_chunks<H / 8>(mine, reinterpret_cast<const T*>(a.g) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                              stg[wid], lane);
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        float o[8];
+        unpack8_w(o, mine[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) A[8 * i + e] = o[e];
+      }
+      if (a.g2)
+        add_row_w<T, NR>(A, reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim, h);
+      if (!valid) {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) A[i] = 0.f;
+      }
+    } else {
+      load_grad_w<T, NR>(A, a, rr, valid, h);
+    }
     if (a.use_ln) {
       const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
       const T* hp = reinterpret_cast<const T*>(a.hpre) + (size_t)rr * H;
@@ -811,10 +855,34 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
         for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? acc[i / 16][i % 16] : 0.f;
       } else if (a.din[0]) {
         gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
-        float v[NR];
-        acc_to_regs<NT, NR>(v, acc);
-        if (a.din_resid[0]) add_grad_w<T, NR>(v, a, rr, h);
-        store_row_w<T, NR>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, v, h, valid);
+        if constexpr (!kStageGradOut) {
+          float v[NR];
+          acc_to_regs<NT, NR>(v, acc);
+          if (a.din_resid[0]) add_grad_w<T, NR>(v, a, rr, h);
+          store_row_w<T, NR>(reinterpret_cast<T*>(a.din[0]) + (size_t)row * H, v, h, valid);
+          continue;
+        }
+        // de = W0^T gpre0 + (g + g2), packed pair by pair for the staged store
+        const T* g1p = a.g ? reinterpret_cast<const T*>(a.g) + (size_t)rr * a.out_dim : nullptr;
+        const T* g2p = a.g2 ? reinterpret_cast<const T*>(a.g2) + (size_t)(a.gidx ? a.gidx[rr] : rr) * a.out_dim
+                            : nullptr;
+        uint4 ob[NR / 8];
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
+          if (a.din_resid[0]) {
+            float x[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, y[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (g1p) load8_w(x, g1p, i, h);
+            if (g2p) load8_w(y, g2p, i, h);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += x[e] + y[e];
+          }
+          ob[i] = pack8_w(o, h);
+        }
+        tile_store_chunks<H / 8>(ob, reinterpret_cast<T*>(a.din[0]) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                                 stg[wid], lane);
       }
     }
   }
