@@ -105,14 +105,17 @@ AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
 // every global access instruction covers 1 KB contiguous. In registers each lane keeps the
 // row's chunks in "exchanged" form: chunk 2i + h of row c (what pack8_w produces).
 template <int NC>
-AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane) {
+AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane,
+                              int ldc = NC) {
+  static_assert(NC >= 8 && NC <= 64, "staged tile I/O needs 8..64 chunks per row");
   constexpr int PER = 64 / NC;  // rows covered by one 1-KB instruction
   const int c = lane & 31, h = lane >> 5;
+  const uint4* gb = reinterpret_cast<const uint4*>(tile_base);
   uint4 raw[32 / PER];
 #pragma unroll
   for (int k = 0; k < 32 / PER; ++k) {
-    const int q = lane + 64 * k;
-    raw[k] = (q / NC < nvalid) ? reinterpret_cast<const uint4*>(tile_base)[q] : uint4{0u, 0u, 0u, 0u};
+    const int q = lane + 64 * k, r = q / NC;
+    raw[k] = (r < nvalid) ? gb[(size_t)r * ldc + q % NC] : uint4{0u, 0u, 0u, 0u};
   }
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
@@ -131,9 +134,12 @@ AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int 
   }
 }
 template <int NC>
-AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane) {
+AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane,
+                               int ldc = NC) {
+  static_assert(NC >= 8 && NC <= 64, "staged tile I/O needs 8..64 chunks per row");
   constexpr int PER = 64 / NC;
   const int c = lane & 31, h = lane >> 5;
+  uint4* gb = reinterpret_cast<uint4*>(tile_base);
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     if ((c >> 3) == p) {
@@ -143,9 +149,9 @@ AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int k = 0; k < 8 / PER; ++k) {
-      const int q = lane + 64 * k;
+      const int q = lane + 64 * k, r = 8 * p + q / NC;
       const uint4 v = stg[q / NC][q % NC];
-      if (8 * p + q / NC < nvalid) reinterpret_cast<uint4*>(tile_base)[(8 * p) * NC + q] = v;
+      if (r < nvalid) gb[(size_t)r * ldc + q % NC] = v;
     }
     __builtin_amdgcn_wave_barrier();
   }

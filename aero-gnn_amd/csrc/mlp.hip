@@ -170,6 +170,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
   constexpr bool IN_FULL = (MODE == M_VEC || MODE == M_NOUT);
   constexpr bool OUT_FULL = (MODE == M_VEC || MODE == M_NIN);
   __shared__ uint4 wl[lds_units<T, NT>()];
+  // 8-row LDS staging of full-width PLAIN inputs / outputs (bf16, H >= 64): measured slower in this
+  // non-persistent kernel (node MLP 0.60 -> 0.73 ms: extra LDS passes + spills), so it is off
+  constexpr bool STAGE = false;
+  __shared__ uint4 stg[STAGE ? WPB : 1][8][STAGE ? 4 * NT : 1];
   const int lane = threadIdx.x & 63;
   const int c = lane & 31, h = lane >> 5;
   const int wave = blockIdx.x * WPB + (threadIdx.x >> 6);
@@ -218,7 +222,23 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       if constexpr (MODE == M_NIN) {
         load_row_narrow<T, NR>(v, reinterpret_cast<const T*>(a.seg[s].ptr) + (size_t)rr * a.seg[s].ld, a.seg[s].k, h);
       } else {
-        load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
+        bool staged = false;
+        if constexpr (STAGE && IN_FULL) {
+          if (a.seg[s].kind == AGN_SEG_PLAIN) {
+            uint4 mine[NR / 8];
+            tile_load_chunks<4 * NT>(mine, reinterpret_cast<const bf16*>(a.seg[s].ptr) + (size_t)wave * 32 * a.seg[s].ld,
+                                     a.rows - wave * 32, stg[threadIdx.x >> 6], lane, a.seg[s].ld / 8);
+#pragma unroll
+            for (int i = 0; i < NR / 8; ++i) {
+              float o[8];
+              unpack8_w(o, mine[i]);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
+            }
+            staged = true;
+          }
+        }
+        if (!staged) load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
       }
       b.set(v);
       __syncthreads();
@@ -271,6 +291,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld + gofs : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld + gofs;
     if constexpr (OUT_FULL) {
+      uint4 ob[STAGE ? NR / 8 : 1];
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float v8[8];
@@ -296,8 +317,12 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
 #pragma unroll
           for (int e = 0; e < 8; ++e) v8[e] = round_t<T>(v8[e]) + r8[e];
         }
-        store8_w(op, i, h, v8, valid);
+        if constexpr (STAGE) ob[i] = pack8_w(v8, h);
+        else store8_w(op, i, h, v8, valid);
       }
+      if constexpr (STAGE)
+        tile_store_chunks<4 * NT>(ob, reinterpret_cast<bf16*>(a.out) + (size_t)wave * 32 * a.out_ld + gofs,
+                                  a.rows - wave * 32, stg[threadIdx.x >> 6], lane, a.out_ld / 8);
     } else {
       // M_NOUT: only the first 32 features (acc tile 0) exist; M_GEN: all, masked
       constexpr int NQ = (MODE == M_NOUT) ? 4 : NR / 4;
