@@ -316,8 +316,18 @@ inline int launch_status() {
 extern "C" {
 
 int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
-  // ~2048 workgroups in flight over all descriptors/blocks, >= 2 LDS stages per split
-  int ns = 1024 / (ndesc_blocks > 0 ? ndesc_blocks : 1);
+  // exactly one full wave of resident workgroups over all descriptors/blocks (no tail wave),
+  // >= 2 LDS stages per split
+  static int resident = 0;
+  if (resident == 0) {
+    int dev = 0, ncu = 256, per = 3;
+    hipDeviceProp_t p;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wgrad_kernel<bf16>, DW_THREADS, 0) != hipSuccess || per < 1)
+      per = 3;
+    resident = ncu * per;
+  }
+  int ns = resident / (ndesc_blocks > 0 ? ndesc_blocks : 1);
   const int maxs = (rows + 2 * DW_ROWS - 1) / (2 * DW_ROWS);
   if (ns > maxs) ns = maxs;
   return ns < 1 ? 1 : ns;
