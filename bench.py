@@ -161,7 +161,8 @@ def main():
 
         def fwd():
             return model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"])
-        workload = (f"BSMS-MGN {S}-scale U-Net train step (fwd+MSE+bwd+allreduce+Adam), "
+        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
+        workload = (f"BSMS-MGN {S}-scale U-Net {what}, "
                     f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU")
         model_name = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
     else:
@@ -170,7 +171,8 @@ def main():
 
         def fwd():
             return model(t["x"], t["edge_attr"], t["edge_index"], multi_data=multi)
-        workload = (f"BSMS-GNN (stale design) 3-level train step (fwd+MSE+bwd+allreduce+Adam), "
+        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
+        workload = (f"BSMS-GNN (stale design) 3-level {what}, "
                     f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU, BFS hierarchy prebuilt")
         model_name = "BSMS_MeshGraphNet(num_levels=3, latent=128, hidden=128, WeightedEdgeConv pooling)"
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
