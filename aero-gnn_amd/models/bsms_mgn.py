@@ -72,7 +72,39 @@ class BiStridedMeshGraphNet(nn.Module):
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
 
     # ------------------------------------------------------------------ hierarchy (index maps)
+    def cache_hierarchy(self, enabled: bool = True, max_entries: int = 64):
+        """Opt-in per-mesh cache of the pooling hierarchy. The reference
+        rebuilds it every forward (bsms_mgn.py:234-256); with the cache a fixed mesh pays the
+        sort/coalesce work once. Keys: tensor identity + version counters + a device fingerprint
+        of edge_index / batch / pos contents (one host sync). Off by default (reference behaviour;
+        bench.py never enables it)."""
+        self._hcache = {} if enabled else None
+        self._hcache_max = max_entries
+        return self
+
+    def _fingerprint(self, edge_index, batch, pos, n):
+        parts = [edge_index[0].double().sum() * 1.000003 + edge_index[1].double().sum() * 0.9999871
+                 + (edge_index[0].double() * edge_index[1].double()).sum() * 1e-7]
+        parts.append(batch.double().sum() if batch is not None else edge_index.new_zeros(()).double())
+        parts.append(pos.double().sum() + (pos.double() ** 2).sum() if pos is not None
+                     else edge_index.new_zeros(()).double())
+        meta = []
+        for t in (edge_index, batch, pos):
+            meta += [None, None, None] if t is None else [t.data_ptr(), t._version, tuple(t.shape)]
+        return (n, tuple(meta), tuple(torch.stack(parts).tolist()))
+
     def _hierarchy(self, edge_index, batch, pos, n):
+        cache = getattr(self, "_hcache", None)
+        if cache is None:
+            return self._build_hierarchy(edge_index, batch, pos, n)
+        key = self._fingerprint(edge_index, batch, pos, n)
+        if key not in cache:
+            if len(cache) >= self._hcache_max:
+                cache.pop(next(iter(cache)))
+            cache[key] = self._build_hierarchy(edge_index, batch, pos, n)
+        return cache[key]
+
+    def _build_hierarchy(self, edge_index, batch, pos, n):
         """Level 0 + one Pooling per down scale (bsms_mgn.py:155-185 order)."""
         level = Level.from_edge_index(edge_index, n)
         ngraph = 1 if batch is None else int(batch[-1].item()) + 1 if n > 0 else 1
