@@ -12,6 +12,11 @@ EU/step is counted from the actual hierarchy (82,432,142 for C3).
 N GPUs (torchrun): every rank trains on its own mesh of the same size (rotation seed = rank),
 one RCCL gradient all-reduce per step: weak scaling, value = total EU / max-rank time.
 
+--config c4 (BASELINE.json configs[3]): a fixed global batch of 64 meshes of
+ellipsoid(400,250) (rotation seed = mesh index) split contiguously over the ranks (64/N each),
+PyG-collated into micro-batches of 8 meshes with gradient accumulation, one all-reduce per step:
+strong scaling.
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -38,7 +43,9 @@ CONFIGS = {
     "c2": (400, 250, 1, torch.float32),
     "c5": (2500, 2000, 6, torch.bfloat16),
     "small": (200, 125, 4, torch.bfloat16),
+    "c4": (400, 250, 4, torch.bfloat16),
 }
+BATCHED = {"c4": (64, 8)}  # config: (global batch of meshes, meshes per micro-batch)
 
 
 def build_model(num_scales, dev):
@@ -61,9 +68,25 @@ def mesh_tensors(nu, nv, seed, dev, dtype):
     return t
 
 
+def collate(parts):
+    """PyG-style collate of equal-layout meshes: concatenated rows, edge_index offset by the
+    running node count, `batch` = mesh index per node."""
+    out, off, eis, bs = {}, 0, [], []
+    for k, p in enumerate(parts):
+        n = p["x"].shape[0]
+        eis.append(p["edge_index"] + off)
+        bs.append(torch.full((n,), k, dtype=torch.long, device=p["x"].device))
+        off += n
+    for key in ("x", "edge_attr", "pos", "y"):
+        out[key] = torch.cat([p[key] for p in parts])
+    out["edge_index"] = torch.cat(eis, 1)
+    out["batch"] = torch.cat(bs)
+    return out
+
+
 def edge_updates(model, t):
     """EU per step = sum over processor layers of the edge count of the level it runs on."""
-    level, pools = model._hierarchy(t["edge_index"], None, t["pos"], t["x"].shape[0])
+    level, pools = model._hierarchy(t["edge_index"], t.get("batch"), t["pos"], t["x"].shape[0])
     E = [level.E] + [p.coarse.E for p in pools]
     nd = len(model.down_layers)
     eu = sum(len(model.down_layers[s]) * E[s] for s in range(nd))
@@ -154,42 +177,64 @@ def main():
     nu, nv, S, dtype = CONFIGS[args.config]
 
     extra = {}
-    if args.model == "bsms_mgn":
+    scaling = "weak"
+    if args.model == "bsms_mgn" and args.config in BATCHED:
+        gb, mb = BATCHED[args.config]
+        if gb % ws:
+            raise SystemExit(f"bench: global batch {gb} is not divisible by {ws} ranks")
+        per = gb // ws
+        seeds = list(range(rank * per, (rank + 1) * per))
+        model, kw = build_model(S, dev)
+        batches = [collate([mesh_tensors(nu, nv, seed=s_, dev=dev, dtype=dtype) for s_ in seeds[i:i + mb]])
+                   for i in range(0, per, mb)]
+        eus = [edge_updates(model, b) for b in batches]
+        eu_step = sum(e for e, _ in eus)
+        Es = eus[0][1]
+        scaling = "strong"
+        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
+        workload = (f"BSMS-MGN {S}-scale U-Net {what}, global batch {gb} meshes of {nu * nv} nodes / "
+                    f"{batches[0]['edge_index'].shape[1] // min(mb, per)} edges, {per} per GPU in micro-batches "
+                    f"of {min(mb, per)} (gradient accumulation)")
+        model_name = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
+        extra["global_batch_meshes"] = gb
+    elif args.model == "bsms_mgn":
         model, kw = build_model(S, dev)
         t = mesh_tensors(nu, nv, seed=rank, dev=dev, dtype=dtype)
+        batches = [t]
         eu_step, Es = edge_updates(model, t)
-
-        def fwd():
-            return model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"])
         what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
         workload = (f"BSMS-MGN {S}-scale U-Net {what}, "
                     f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU")
         model_name = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
     else:
         model, t, multi, eu_step, Es, prep_ms = setup_bsms_gnn(nu, nv, rank, dev, dtype)
+        batches = [t]
         extra["preprocess_ms"] = round(prep_ms, 1)
-
-        def fwd():
-            return model(t["x"], t["edge_attr"], t["edge_index"], multi_data=multi)
         what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
         workload = (f"BSMS-GNN (stale design) 3-level {what}, "
                     f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU, BFS hierarchy prebuilt")
         model_name = "BSMS_MeshGraphNet(num_levels=3, latent=128, hidden=128, WeightedEdgeConv pooling)"
+
+    def fwd(b):
+        if args.model == "bsms_mgn":
+            return model(b["x"], b["edge_attr"], b["edge_index"], batch=b.get("batch"), pos=b["pos"])
+        return model(b["x"], b["edge_attr"], b["edge_index"], multi_data=multi)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     allreduce = D.GradAllReduce(model.parameters())
-    n_glob = D.global_count(t["y"].numel(), dev)
+    n_glob = D.global_count(sum(b["y"].numel() for b in batches), dev)
 
     def step():
         if args.mode == "train":
-            pred = fwd()
-            loss = D.mse_sum_loss(pred, t["y"], n_glob)
-            loss.backward()
+            for b in batches:  # gradient accumulation over micro-batches (sum loss / global count)
+                loss = D.mse_sum_loss(fwd(b), b["y"], n_glob)
+                loss.backward()
             allreduce()
             opt.step()
             opt.zero_grad(set_to_none=True)
         else:
             with torch.no_grad():
-                fwd()
+                for b in batches:
+                    fwd(b)
 
     for _ in range(args.warmup):
         step()
@@ -251,13 +296,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": dname,
         "data": "synthetic ellipsoid aero surface mesh (aerognn.meshgen), random-init weights (seed 0)",
         "config": {"workload": workload, "model": model_name, **extra,
                    "mode": args.mode, "edge_updates_per_step_per_gpu": eu_step, "level_edges": Es,
-                   "global_batch": ws, "parallelism": f"dp{ws}"},
+                   "global_batch": extra.get("global_batch_meshes", ws), "parallelism": f"dp{ws}"},
         "roofline": roof,
         "kernels": kernels,
     }
