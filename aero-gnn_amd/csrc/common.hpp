@@ -104,8 +104,12 @@ AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
 // through an 8-row LDS staging area `stg` (8 x NC uint4, private to the wave) in 4 passes, so
 // every global access instruction covers 1 KB contiguous. In registers each lane keeps the
 // row's chunks in "exchanged" form: chunk 2i + h of row c (what pack8_w produces).
+// Staging rows are padded by STG_PAD chunks: with a 256-B stride the 16 (row, half) addresses
+// one wave touches per chunk step all fall into the same 4 banks (8-way conflicts, measured
+// 1.6e8 SQ_LDS_BANK_CONFLICT cycles per 3 edge forwards); 288 B spreads them over 64 banks.
+constexpr int STG_PAD = 2;
 template <int NC>
-AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane,
+AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC + STG_PAD], int lane,
                               int ldc = NC) {
   static_assert(NC >= 8 && NC <= 64, "staged tile I/O needs 8..64 chunks per row");
   constexpr int PER = 64 / NC;  // rows covered by one 1-KB instruction
@@ -134,7 +138,7 @@ AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int 
   }
 }
 template <int NC>
-AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC], int lane,
+AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC + STG_PAD], int lane,
                                int ldc = NC) {
   static_assert(NC >= 8 && NC <= 64, "staged tile I/O needs 8..64 chunks per row");
   constexpr int PER = 64 / NC;

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
   // 8-row LDS staging of full-width PLAIN inputs / outputs (bf16, H >= 64): measured slower in this
   // non-persistent kernel (node MLP 0.60 -> 0.73 ms: extra LDS passes + spills), so it is off
   constexpr bool STAGE = false;
-  __shared__ uint4 stg[STAGE ? WPB : 1][8][STAGE ? 4 * NT : 1];
+  __shared__ uint4 stg[STAGE ? WPB : 1][8][STAGE ? 4 * NT + STG_PAD : 1];
   const int lane = threadIdx.x & 63;
   const int c = lane & 31, h = lane >> 5;
   const int wave = blockIdx.x * WPB + (threadIdx.x >> 6);
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
-  __shared__ uint4 stg[RES_WPB][8][H / 8];  // per-wave 8-row staging: coalesced e' stores
+  __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e' stores
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ float lnp[RES_WPB][2][H];
   __shared__ __attribute__((aligned(16))) float pg_lds[H];  // LN gamma
-  __shared__ uint4 stg[RES_WPB][8][H / 8];  // per-wave 8-row staging: coalesced g / de
+  __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced g / de
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
   for (int i = threadIdx.x; i < H; i += RES_BLOCK) pg_lds[i] = a.use_ln ? a.ln_g[i] : 0.f;
   __syncthreads();

@@ -68,20 +68,15 @@ def mesh_tensors(nu, nv, seed, dev, dtype):
     return t
 
 
-def collate(parts):
-    """PyG-style collate of equal-layout meshes: concatenated rows, edge_index offset by the
-    running node count, `batch` = mesh index per node."""
-    out, off, eis, bs = {}, 0, [], []
-    for k, p in enumerate(parts):
-        n = p["x"].shape[0]
-        eis.append(p["edge_index"] + off)
-        bs.append(torch.full((n,), k, dtype=torch.long, device=p["x"].device))
-        off += n
-    for key in ("x", "edge_attr", "pos", "y"):
-        out[key] = torch.cat([p[key] for p in parts])
-    out["edge_index"] = torch.cat(eis, 1)
-    out["batch"] = torch.cat(bs)
-    return out
+def batch_tensors(nu, nv, seeds, dev, dtype):
+    """PyG-style collate (aerognn.meshgen.collate: concatenated rows, edge_index offset by the
+    running node count, `batch` = mesh index per node) of one mesh per seed, on the device."""
+    from aerognn.meshgen import collate, ellipsoid
+    b = collate([ellipsoid(nu, nv, seed=s) for s in seeds])
+    t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
+    for k in ("x", "edge_attr"):
+        t[k] = t[k].to(dtype)
+    return t
 
 
 def edge_updates(model, t):
@@ -185,8 +180,7 @@ def main():
         per = gb // ws
         seeds = list(range(rank * per, (rank + 1) * per))
         model, kw = build_model(S, dev)
-        batches = [collate([mesh_tensors(nu, nv, seed=s_, dev=dev, dtype=dtype) for s_ in seeds[i:i + mb]])
-                   for i in range(0, per, mb)]
+        batches = [batch_tensors(nu, nv, seeds[i:i + mb], dev, dtype) for i in range(0, per, mb)]
         eus = [edge_updates(model, b) for b in batches]
         eu_step = sum(e for e, _ in eus)
         Es = eus[0][1]

@@ -13,4 +13,4 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/ctr_$i -o m -- \
       python tools/layer_micro.py 2 > gpurun_out/ctr_$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/ctr_$i.log; }
 done
-python tools/pmc_summary.py "res_kernel|wgrad_kernel|segment_sum" gpurun_out/ctr_* > gpurun_out/ctr_summary.txt
+python tools/pmc_summary.py "${KFILTER:-res_kernel|wgrad_kernel|segment_sum}" gpurun_out/ctr_* > gpurun_out/ctr_summary.txt
