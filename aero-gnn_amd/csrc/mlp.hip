@@ -757,7 +757,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
   __shared__ float lnp[RES_WPB][2][H];
   __shared__ __attribute__((aligned(16))) float pg_lds[H];  // LN gamma
   __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced g / de
-  for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
+  // layer 0's weights only serve dX: an encoder (narrow input, no input gradient) skips them
+  // (res_bwd_ok: without dX every din pointer is NULL; with dX there is exactly one segment)
+  for (int l = a.din[0] ? 0 : 1; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wtpk[l], NUH, 0, NT, 0, NUH);
   for (int i = threadIdx.x; i < H; i += RES_BLOCK) pg_lds[i] = a.use_ln ? a.ln_g[i] : 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -1062,8 +1064,12 @@ bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
          a->seg[0].ld % 8 == 0 && a->rows >= 64 * 1024;
 }
 bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
+  // edge/node chains with an H-wide dX, or any chain without dX (the edge encoder: d_e = 4 in)
+  bool need_dx = false;
+  for (int s = 0; s < a->din_nseg; ++s) need_dx |= a->din[s] != nullptr;
+  const bool din_ok = need_dx ? (a->din_nseg == 1 && a->in_dim == 128 && a->din_k[0] == 128) : a->nlin > 1;
   return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
-         a->in_dim == 128 && a->din_nseg == 1 && a->din_k[0] == 128 && a->rows >= 64 * 1024;
+         din_ok && a->rows >= 64 * 1024;
 }
 }  // namespace
 

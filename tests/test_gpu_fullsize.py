@@ -73,6 +73,34 @@ def test_resident_kernels_bitwise_equal_general():
     assert worst <= 1e-6
 
 
+def test_resident_encoder_backward_bitwise_equal_general():
+    """The edge encoder (MLP 4 -> 128, n_hid=2, LN; no input gradient) takes the resident
+    backward too: gpre / parameter grads match the general kernel."""
+    from models.mlp import MLP
+    E = 100_000
+    g = torch.Generator(device="cpu").manual_seed(3)
+    ea = torch.randn(E, 4, generator=g).to(DEV, torch.bfloat16)
+    gy = torch.randn(E, 128, generator=g).to(DEV, torch.bfloat16)
+    torch.manual_seed(0)
+    enc = MLP(4, 128, 128, num_hidden_layers=2).to(DEV)
+    outs = []
+    old = _set_resident(1)
+    try:
+        for flag in (1, 0):
+            _set_resident(flag)
+            enc.zero_grad()
+            y = enc(ea)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), {n: p.grad.clone() for n, p in enc.named_parameters()}))
+    finally:
+        _set_resident(old)
+    assert torch.equal(outs[0][0], outs[1][0])
+    worst = max(rel_l2(outs[0][1][n].float(), outs[1][1][n].double()) for n in outs[0][1])
+    print(f"encoder param grads worst rel-L2 {worst:.2e}")
+    assert worst <= 1e-6
+
+
 def test_c2_layer_fp32_vs_oracle():
     from aerognn.graph import Level
     from models.mgnLayer import MeshGraphNetLayer
