@@ -35,7 +35,8 @@ class MlpFwdArgs(C.Structure):
                 ("ln_g", vp), ("ln_b", vp),
                 ("proj", vp), ("src", vp), ("dst", vp),
                 ("resid", vp), ("out", vp),
-                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32)]
+                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32),
+                ("mask", vp * MAX_LIN)]
 
 
 class MlpBwdArgs(C.Structure):
@@ -47,7 +48,8 @@ class MlpBwdArgs(C.Structure):
                 ("gpre", vp * MAX_LIN),
                 ("din_nseg", i32), ("din_k", i32 * MAX_SEG),
                 ("din", vp * MAX_SEG), ("din_resid", i32 * MAX_SEG),
-                ("ln_partial", vp), ("tiled", i32), ("gpre_tiled", i32)]
+                ("ln_partial", vp), ("tiled", i32), ("gpre_tiled", i32),
+                ("mask", vp * MAX_LIN)]
 
 
 MAX_WGRAD = 8

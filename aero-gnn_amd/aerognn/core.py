@@ -63,6 +63,19 @@ def tiled_empty(rows, width, dtype, device):
     return t
 
 
+def relu_mask_empty(rows, width, device):
+    """AGN_RELU_MASK buffer (aerognn.h) for a [rows, width] ReLU output: max(1, width / 64)
+    dwords per lane of each 32-row tile."""
+    nd = max(1, (width + 63) // 64)
+    return torch.empty((rows + 31) // 32 * nd * 64, dtype=torch.int32, device=device)
+
+
+def _mask_of(t):
+    """The backward reads ReLU sign bits (AGN_RELU_MASK, attached to each saved activation by
+    the allocator) instead of the activations, which are saved for agn_wgrad only."""
+    return getattr(t, "agn_mask", None)
+
+
 def is_tiled(t) -> bool:
     return t is not None and getattr(t, "agn_tiled", False)
 
@@ -191,6 +204,7 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
     if acts is not None:
         for i, t in enumerate(acts):
             a.act[i] = ptr(t)
+            a.mask[i] = ptr(_mask_of(t))
     a.hpre, a.stats = ptr(hpre), ptr(stats)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
     with timed(tag, cost):
@@ -214,6 +228,7 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
         a.gpre[i] = ptr(gpre[i]) if gpre[i] is not None else None
     for i, t in enumerate(acts):
         a.act[i] = ptr(t)
+        a.mask[i] = ptr(_mask_of(t))
     a.hpre, a.stats, a.ln_g = ptr(hpre), ptr(stats), ln_g
     a.g, a.g2, a.gidx = ptr(g), ptr(g2), ptr(gidx)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
@@ -312,14 +327,19 @@ class WGrad:
 
 
 # --------------------------------------------------------------------------- algorithmic costs
+def mask_bytes(H):
+    """AGN_RELU_MASK bytes per row of one hidden layer (8 B per lane pair and dword)."""
+    return 8 * max(1, (H + 63) // 64)
+
+
 def cost_edge_fwd(E, N, H, s, nlin, train):
     """Minimum HBM bytes / MFMA flops of one fused edge-MLP launch."""
-    per = 2 * H * s + 8 + ((nlin - 1) * H * s + H * s + 8 if train else 0)
+    per = 2 * H * s + 8 + ((nlin - 1) * (H * s + mask_bytes(H)) + H * s + 8 if train else 0)
     return E * per + N * 2 * H * s, 2 * E * H * H * nlin
 
 
 def cost_node_fwd(E, N, H, s, nlin, train):
-    per = 2 * H * s + 8 + ((nlin - 1) * H * s + 2 * H * s + 8 if train else 0)
+    per = 2 * H * s + 8 + ((nlin - 1) * (H * s + mask_bytes(H)) + 2 * H * s + 8 if train else 0)
     return N * per + E * H * s, 2 * N * H * (2 * H + (nlin - 1) * H)
 
 
@@ -328,18 +348,19 @@ def cost_proj(N, H, s):
 
 
 def cost_edge_bwd(E, N, H, s, nlin):
-    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + H * s + 4
+    # g, g2[dst], masks, hpre, stats, gpre writes, de, dst index
+    per = H * s + H * s + (nlin - 1) * mask_bytes(H) + H * s + 8 + nlin * H * s + H * s + 4
     return E * per + N * H * s, 2 * E * H * H * nlin
 
 
 def cost_edge_fwd_cat(E, N, H, s, nlin, train):
     """Concat edge MLP (EdgeBlock / GMP): e and the two gathered node rows in, e' (+ saves) out."""
-    per = 4 * H * s + 8 + ((nlin - 1) * H * s + H * s + 8 if train else 0)
+    per = 4 * H * s + 8 + ((nlin - 1) * (H * s + mask_bytes(H)) + H * s + 8 if train else 0)
     return E * per, 2 * E * H * (3 * H + (nlin - 1) * H)
 
 
 def cost_edge_bwd_cat(E, N, H, s, nlin):
-    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + 3 * H * s + 4
+    per = H * s + H * s + (nlin - 1) * mask_bytes(H) + H * s + 8 + nlin * H * s + 3 * H * s + 4
     return E * per + N * H * s, 2 * E * H * (3 * H + (nlin - 1) * H)
 
 
@@ -356,5 +377,5 @@ def cost_wec_bwd(E, N, out, s, hid=64):
 
 
 def cost_node_bwd(N, H, s, nlin):
-    per = H * s + H * s + (nlin - 1) * H * s + 8 + nlin * H * s + 2 * H * s
+    per = H * s + H * s + (nlin - 1) * mask_bytes(H) + 8 + nlin * H * s + 2 * H * s  # g, hpre, masks, ...
     return N * per, 2 * N * H * (H * (nlin - 1) + 2 * H)

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, bwd_nblocks, tiled_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+from .core import (Pack, WGrad, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_sum, stream)
@@ -104,6 +104,8 @@ def _alloc_saves(spec, rows, dtype, dev, train):
         return None, None, None
     emp = tiled_empty if spec.tiled_saves else (lambda r, w, dt, d: torch.empty(r, w, dtype=dt, device=d))
     acts = [emp(rows, spec.hidden, dtype, dev) for _ in range(spec.nlin - 1)]
+    for t in acts:  # sign bits for the backward (AGN_RELU_MASK); the rows stay for agn_wgrad
+        t.agn_mask = relu_mask_empty(rows, spec.hidden, dev)
     hpre = stats = None
     if spec.ln is not None:
         hpre = emp(rows, spec.out_dim, dtype, dev)

@@ -431,6 +431,67 @@ template <int NR> struct BOp<float, NR> {
 // The number of activation registers for K features is nrk(K) = 8 * ceil(K/16).
 template <typename T> AGN_DEV constexpr int units_k(int k) { return nrk(k) / BOp<T, 16>::RPU; }
 
+// ---------------------------------------------------------------- AGN_RELU_MASK (aerognn.h)
+// The backward only needs sign(relu output) of a hidden layer: one bit per activation register.
+// Dword d of lane `lane` in 32-row tile t sits at (t * ND + d) * 64 + lane (one 256-B coalesced
+// access per dword); bit j = register 32d + j of the packed operand is > 0 (the stored value,
+// i.e. after rounding to T, exactly the test the backward applied to the re-read activation).
+template <int NR> AGN_DEV constexpr int mask_dwords() { return (NR + 31) / 32; }
+// bit i = (register i > 0). bf16: integer tests on the packed pairs (a bf16 in the top 16 bits of
+// a dword is > 0 as a signed int iff it is a positive nonzero value), no float conversions.
+template <int NR> AGN_DEV bool bop_pos(const BOp<bf16, NR>& b, int i) {
+  const uint32_t w = __builtin_bit_cast(u32x4, b.u[i / 8])[(i % 8) / 2];
+  return (int32_t)((i & 1) ? (w & 0xffff0000u) : (w << 16)) > 0;
+}
+template <int NR> AGN_DEV bool bop_pos(const BOp<float, NR>& b, int i) { return b.u[i] > 0.f; }
+template <typename T, int NR>
+AGN_DEV void store_relu_mask(void* base, const BOp<T, NR>& b, int tile, int lane) {
+  constexpr int ND = mask_dwords<NR>();
+  uint32_t* p = reinterpret_cast<uint32_t*>(base) + (size_t)tile * ND * 64 + lane;
+  if constexpr (sizeof(T) == 2) {
+    // relu outputs are >= 0 or -0: per bf16 half, (magnitude + 0x7fff) carries into the sign
+    // position iff the magnitude is nonzero; & ~sign drops -0. Bits are placed with v_bfe +
+    // v_lshl_or (inline shift constants: no per-bit literal masks held in VGPRs).
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int i = 32 * d + 2 * k;  // registers i, i+1 share one packed dword
+        if (i < NR) {
+          const uint32_t x = __builtin_bit_cast(u32x4, b.u[i / 8])[(i % 8) / 2];
+          const uint32_t q = ((x & 0x7fff7fffu) + 0x7fff7fffu) & ~x;
+          w |= __builtin_amdgcn_ubfe(q, 15, 1) << (2 * k);
+          w |= __builtin_amdgcn_ubfe(q, 31, 1) << (2 * k + 1);
+        }
+      }
+      p[d * 64] = w;
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (32 * d + j < NR) w |= (bop_pos<NR>(b, 32 * d + j) ? 1u : 0u) << j;
+      p[d * 64] = w;
+    }
+  }
+}
+template <int NR>
+AGN_DEV void load_relu_mask(uint32_t (&m)[mask_dwords<NR>()], const void* base, int tile, int lane) {
+  constexpr int ND = mask_dwords<NR>();
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(base) + (size_t)tile * ND * 64 + lane;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) m[d] = p[d * 64];
+}
+// v * bit i of the mask (the relu backward select): v_bfe_i32 gives 0 / all-ones, then an AND of
+// the float's bits (no per-bit literal constants, no compares)
+AGN_DEV float mask_sel(const uint32_t* m, int i, float v) {
+  const int32_t s = __builtin_amdgcn_sbfe((int32_t)m[i >> 5], i & 31, 1);
+  return __uint_as_float(__float_as_uint(v) & (uint32_t)s);
+}
+
 // acc[ot] += A[ot tile, units 0..nu-1] * B, A fragments staged in LDS as [ot][ku_total][64]
 // (16 B per lane, linear: one conflict-free ds_read_b128 per lane per unit). The next unit's
 // fragments are read while the current unit's MFMAs issue.

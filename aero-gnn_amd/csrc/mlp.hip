@@ -259,6 +259,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
         else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       }
+      if (a.mask[l - 1]) store_relu_mask<T, NR>(a.mask[l - 1], b, wave, lane);
       if (OUT_FULL || !last) acc_bias<NT, true>(acc, a.bias[l], H, h);
       else acc_bias<NT, false>(acc, a.bias[l], outl, h);
       __syncthreads();
@@ -493,13 +494,13 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
       __syncthreads();
       gemm<T, NT, NR, true>(acc, b, kuM, wl, kuM, NT, lane);
-      float m[NR];
       cbarrier();
-      if (a.tiled) load_row_tiled<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]), rr, h);
-      else load_row<T, NR, true>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, H, h);
       acc_to_regs<NT, NR>(A, acc);
+      // AGN_RELU_MASK sign bits (8 B per lane instead of the activation row)
+      uint32_t mk[mask_dwords<NR>()];
+      load_relu_mask<NR>(mk, a.mask[l - 1], wave, lane);
 #pragma unroll
-      for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? A[i] : 0.f;
+      for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, A[i]);
     } else {
       int koff = 0;
       for (int s = 0; s < a.din_nseg; ++s) {
@@ -646,6 +647,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
         else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       }
+      if (a.mask[l - 1]) store_relu_mask<T, NR>(a.mask[l - 1], b, tile, lane);
+      cbarrier();
       acc_bias_lds<NT>(acc, pv[l], h);
       gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
     }
@@ -874,12 +877,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
       if (l > 0) {
+        // AGN_RELU_MASK sign bits (res_bwd_ok: always given), issued before the MFMAs
+        uint32_t mk[mask_dwords<NR>()];
+        load_relu_mask<NR>(mk, a.mask[l - 1], tile, lane);
         gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
-        float m[NR];
-        if (a.tiled) load_row_tiled<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]), rr, h);
-        else load_row_w<T, NR>(m, reinterpret_cast<const T*>(a.act[l - 1]) + (size_t)rr * H, h);
 #pragma unroll
-        for (int i = 0; i < NR; ++i) A[i] = (m[i] > 0.f) ? acc[i / 16][i % 16] : 0.f;
+        for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, acc[i / 16][i % 16]);
       } else if (a.din[0]) {
         gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
         if constexpr (!kStageGradOut) {
@@ -1054,7 +1057,7 @@ bool fwd_ptrs_aligned(const agn_mlp_fwd_args* a) {
 bool bwd_ptrs_aligned(const agn_mlp_bwd_args* a) {
   bool ok = al16(a->g) && al16(a->g2) && al16(a->hpre);
   for (int s = 0; s < a->din_nseg; ++s) ok = ok && al16(a->din[s]);
-  for (int l = 0; l < a->nlin; ++l) ok = ok && al16(a->act[l]) && al16(a->gpre[l]);
+  for (int l = 0; l < a->nlin; ++l) ok = ok && al16(a->gpre[l]);
   return ok;
 }
 int g_opt_resident = 1;
@@ -1156,8 +1159,8 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
     if (a->din_k[s] > a->hidden) return AGN_E_SHAPE;
     if (s + 1 < a->din_nseg && (a->din_k[s] % 32) != 0) return AGN_E_SHAPE;
   }
-  for (int l = 0; l < a->nlin; ++l)
-    if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
+  for (int l = 0; l + 1 < a->nlin; ++l)
+    if (!a->mask[l]) return AGN_E_ARG;  // the ReLU backward reads the sign bits (AGN_RELU_MASK)
   int mode = M_GEN;
   if (bwd_ptrs_aligned(a)) {
     if (a->out_dim == a->hidden) mode = M_VEC;

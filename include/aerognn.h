@@ -80,6 +80,7 @@ typedef struct {
   float* stats;                    /* [rows][2] = mean, rstd */
   int tiled;                       /* 1: act/hpre in the tiled layout (AGN_TILED below, hidden-wide) */
   int _pad2;
+  void* mask[AGN_MAX_LIN];         /* optional AGN_RELU_MASK of act[l] (may be given without act[l]) */
 } agn_mlp_fwd_args;
 
 typedef struct {
@@ -92,7 +93,7 @@ typedef struct {
   int use_ln;
   int ln_rows;     /* out: rows of ln_partial written (<= agn_mlp_bwd_nwaves(rows)) */
   const void* wtpk[AGN_MAX_LIN];   /* packed TRANSPOSED weights (agn_pack, trans = 1) */
-  const void* act[AGN_MAX_LIN];
+  const void* act[AGN_MAX_LIN];    /* not read (the ReLU backward uses mask[] below); kept for the layout */
   const void* hpre;
   const float* stats;
   const float* ln_g;
@@ -110,6 +111,7 @@ typedef struct {
   float* ln_partial;               /* [agn_mlp_bwd_nwaves(rows)][2][out_dim]: sum g*xhat, sum g */
   int tiled;                       /* 1: act/hpre are read in the tiled layout */
   int gpre_tiled;                  /* bit l: gpre[l] written in the tiled layout (hidden-wide only) */
+  const void* mask[AGN_MAX_LIN];   /* AGN_RELU_MASK of hidden layer l < nlin-1 (required) */
 } agn_mlp_bwd_args;
 
 /* AGN_TILED layout of a [rows][H] activation saved for the backward (H = hidden, rows padded to
@@ -118,6 +120,13 @@ typedef struct {
  * U = H * elem_size / 16; for bf16 it holds features 16i+4h+{0..3} and 16i+8+4h+{0..3}, for fp32
  * features 8i+4h+{0..3}. One wave store/load instruction moves 1 KB contiguous. Only libaerognn
  * kernels read it (the MLP backward and agn_wgrad). */
+
+/* AGN_RELU_MASK of a [rows][H] ReLU output (rows padded to 32): the sign bits the backward needs
+ * instead of the activation. Per 32-row tile, ND = max(1, H / 64) dwords per lane of the producing
+ * wave, dword (tile t, d, lane) at 4-B index (t * ND + d) * 64 + lane; bit j of dword d is
+ * (activation register 32 d + j > 0) in the register order of AGN_TILED (register rho of lane
+ * (row r % 32, half h) holds feature 8 (rho / 4) + 4 h + rho % 4). 16 B per row at H = 128
+ * instead of 256 B. Only libaerognn kernels read it. */
 
 /* Pack an A operand A[r][k] = trans ? W[k][r] : W[r][k] (r < rows, k < cols) into rows
  * [row_off, row_off+rows) x cols [col_off, col_off+cols) of a packed [dst_rows x dst_cols]

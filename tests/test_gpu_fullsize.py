@@ -171,3 +171,58 @@ def test_c3_train_step_deterministic_and_finite():
     assert torch.equal(outs[0][0], outs[1][0])
     for a, b in zip(outs[0][1], outs[1][1]):
         assert torch.isfinite(a).all() and torch.equal(a, b)
+
+
+
+def _decode_tiled(t, rows, H):
+    """AGN_TILED [rows_pad, H] -> row-major [rows, H] (aerognn.h layout): bf16 unit (i, h) of row c
+    holds features 16i+4h+{0..3}, 16i+8+4h+{0..3}; fp32 unit (i, h) features 8i+4h+{0..3}."""
+    if t.dtype == torch.bfloat16:
+        U, per, iv = H * 2 // 16, 8, torch.int16
+    else:
+        U, per, iv = H * 4 // 16, 4, torch.int32
+    u = t.view(iv).reshape(-1, U, 2, 32, per)  # [tile][i][h][c][per]
+    out = torch.empty(u.shape[0], 32, H, dtype=iv, device=t.device)
+    for i in range(U):
+        for hh in range(2):
+            v = u[:, i, hh]
+            if per == 8:
+                out[:, :, 16 * i + 4 * hh:16 * i + 4 * hh + 4] = v[:, :, :4]
+                out[:, :, 16 * i + 8 + 4 * hh:16 * i + 8 + 4 * hh + 4] = v[:, :, 4:]
+            else:
+                out[:, :, 8 * i + 4 * hh:8 * i + 4 * hh + 4] = v
+    return out.reshape(-1, H)[:rows].view(t.dtype)
+
+
+@pytest.mark.parametrize("rows", [100_000, 3_000])  # resident / general forward
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_relu_mask_matches_saved_activations(rows, dtype):
+    """AGN_RELU_MASK bits written by the forward == (saved activation > 0) for every hidden layer:
+    the backward's ReLU select reads these bits instead of the activations."""
+    from models.mlp import MLP
+    H = 128
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(rows, H, generator=g).to(DEV, dtype)
+    torch.manual_seed(0)
+    mlp = MLP(H, H, H, num_hidden_layers=2).to(DEV)
+    y = mlp(x.requires_grad_(True))
+    ctx = y.grad_fn
+    torch.cuda.synchronize()
+    assert len(ctx.acts) == 2
+    for act in ctx.acts:
+        if getattr(act, "agn_tiled", False):
+            a = _decode_tiled(act, rows, H).float()
+        else:
+            a = act[:rows].float()
+        pos = (a > 0).cpu().numpy()  # [rows, H]
+        ntile = (rows + 31) // 32
+        m = act.agn_mask.cpu().numpy().astype(np.uint32).reshape(ntile, 2, 64)  # [tile][d][lane]
+        rho = np.arange(64)
+        bits = (m[:, rho // 32, :] >> (rho % 32)[None, :, None]) & 1  # [tile][rho][lane]
+        lane = np.arange(64)
+        c, h = lane % 32, lane // 32
+        f = 8 * (rho[:, None] // 4) + 4 * h[None, :] + rho[:, None] % 4  # [rho][lane]
+        r = (np.arange(ntile)[:, None, None] * 32 + c[None, None, :]).repeat(64, 1)  # [tile][rho][lane]
+        ok = r < rows
+        expect = pos[np.minimum(r, rows - 1), np.broadcast_to(f, r.shape)]
+        assert np.array_equal(bits.astype(bool)[ok], expect[ok])
