@@ -259,7 +259,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
         else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       }
-      if (a.mask[l - 1]) store_relu_mask<T, NR>(a.mask[l - 1], b, wave, lane);
+      // waves past the last 32-row tile (the grid rounds up to WPB waves) own no mask tile
+      if (a.mask[l - 1] && wave * 32 < a.rows) store_relu_mask<T, NR>(a.mask[l - 1], b, wave, lane);
       if (OUT_FULL || !last) acc_bias<NT, true>(acc, a.bias[l], H, h);
       else acc_bias<NT, false>(acc, a.bias[l], outl, h);
       __syncthreads();
@@ -498,7 +499,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       acc_to_regs<NT, NR>(A, acc);
       // AGN_RELU_MASK sign bits (8 B per lane instead of the activation row)
       uint32_t mk[mask_dwords<NR>()];
-      load_relu_mask<NR>(mk, a.mask[l - 1], wave, lane);
+      load_relu_mask<NR>(mk, a.mask[l - 1], min(wave, (a.rows - 1) / 32), lane);  // clamp: idle waves
 #pragma unroll
       for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, A[i]);
     } else {

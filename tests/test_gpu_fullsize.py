@@ -178,9 +178,9 @@ def _decode_tiled(t, rows, H):
     """AGN_TILED [rows_pad, H] -> row-major [rows, H] (aerognn.h layout): bf16 unit (i, h) of row c
     holds features 16i+4h+{0..3}, 16i+8+4h+{0..3}; fp32 unit (i, h) features 8i+4h+{0..3}."""
     if t.dtype == torch.bfloat16:
-        U, per, iv = H * 2 // 16, 8, torch.int16
+        U, per, iv = H // 16, 8, torch.int16  # 16-B units per lane (half row)
     else:
-        U, per, iv = H * 4 // 16, 4, torch.int32
+        U, per, iv = H // 8, 4, torch.int32
     u = t.view(iv).reshape(-1, U, 2, 32, per)  # [tile][i][h][c][per]
     out = torch.empty(u.shape[0], 32, H, dtype=iv, device=t.device)
     for i in range(U):
@@ -208,7 +208,7 @@ def test_relu_mask_matches_saved_activations(rows, dtype):
     y = mlp(x.requires_grad_(True))
     ctx = y.grad_fn
     torch.cuda.synchronize()
-    assert len(ctx.acts) == 2
+    assert len(ctx.acts) == 3  # num_hidden_layers=2: Lin, 2 hidden Lin, out Lin -> 3 ReLU outputs
     for act in ctx.acts:
         if getattr(act, "agn_tiled", False):
             a = _decode_tiled(act, rows, H).float()
