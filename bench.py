@@ -159,7 +159,7 @@ def main():
                     help="bsms_mgn: BiStridedMeshGraphNet (the headline); bsms_gnn: the stale BSMS_MeshGraphNet")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                                      "r1_pmc_traffic.json"),
+                                                      "r1e_pmc_traffic.json"),
                     help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels")
     args = ap.parse_args()
 
