@@ -82,9 +82,52 @@ class PackDesc(C.Structure):
 
 _lib = None
 
+# Entry points that enqueue device work on a stream. When core.PROF is a list, every call of one
+# of them is bracketed by HIP events on the caller's current stream (the stream the launch goes
+# to) and recorded under its name, unless an enclosing core.timed(...) already times it under a
+# finer tag (edge_fwd, node_bwd, ...). Nothing is recorded when PROF is None.
+LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_partials", "agn_wgrad", "agn_colsum",
+            "agn_segment_sum", "agn_gather_rows", "agn_radix_sort_u64", "agn_row_ptr", "agn_row_ptr_i64",
+            "agn_exclusive_scan_i32", "agn_pool_sort_keys", "agn_pool_assign", "agn_pool_edge_candidates",
+            "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
+            "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
+            "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_collate",
+            "agn_global_pool", "agn_mlp_bwd_fused")
+
 
 class AeroGNNError(RuntimeError):
     pass
+
+
+class _Lib:
+    """The loaded CDLL; launch entry points go through the optional event timer."""
+
+    def __init__(self, cdll):
+        self._cdll = cdll
+        for name in LAUNCHES:
+            if hasattr(cdll, name):
+                setattr(self, name, _timed_launch(getattr(cdll, name), name[4:]))
+
+    def __getattr__(self, name):
+        return getattr(self._cdll, name)
+
+
+def _timed_launch(f, tag):
+    from . import core
+
+    def call(*args):
+        prof = core.PROF
+        if prof is None or core._TIMED_DEPTH:
+            return f(*args)
+        import torch
+        s = torch.cuda.Event(enable_timing=True)
+        s.record()
+        rc = f(*args)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        prof.append((tag, None, s, e))
+        return rc
+    return call
 
 
 def lib():
@@ -140,7 +183,7 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
-        _lib = L
+        _lib = _Lib(L)
     return _lib
 
 

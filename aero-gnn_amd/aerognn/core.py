@@ -19,26 +19,35 @@ def stream():
 # --------------------------------------------------------------------------- launch timing
 # When PROF is a list, every tagged kernel launch is bracketed by HIP events recorded on the
 # stream it runs on (torch's current stream): entries (tag, (alg_bytes, alg_flops), start, end).
+# Untagged launches are recorded under their entry-point name by _lib (see _lib.LAUNCHES).
 PROF = None
+_TIMED_DEPTH = 0
 
 
 class _Timed:
-    __slots__ = ("tag", "cost", "s")
+    __slots__ = ("tag", "cost", "s", "on")
 
     def __init__(self, tag, cost):
         self.tag, self.cost = tag, cost
+        self.on = False
 
     def __enter__(self):
+        global _TIMED_DEPTH
         if PROF is not None and self.tag is not None:
+            self.on = True
+            _TIMED_DEPTH += 1
             self.s = torch.cuda.Event(enable_timing=True)
             self.s.record()
         return self
 
     def __exit__(self, *a):
-        if PROF is not None and self.tag is not None:
+        global _TIMED_DEPTH
+        if self.on:
+            _TIMED_DEPTH -= 1
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            PROF.append((self.tag, self.cost, self.s, e))
+            if PROF is not None:
+                PROF.append((self.tag, self.cost, self.s, e))
         return False
 
 
@@ -327,6 +336,25 @@ class WGrad:
 
 
 # --------------------------------------------------------------------------- algorithmic costs
+# Each tagged launch records (alg_bytes, flops, impl_bytes):
+#   alg_bytes  = the launch's share of SURVEY §8(d)'s fully-fused per-layer minimum
+#                B = E(2sH + 8) + N(8sH): edge kernel E(2sH + 8) + N(2sH) (P_s/P_d rows read once),
+#                projection N(3sH) (read x, write P_s|P_d), node kernel N(3sH) (read x, agg, write x');
+#                training = 3x forward, so each backward kernel carries 2x its forward share;
+#   impl_bytes = the bytes this implementation's kernel must move (its own I/O model, cost_* below).
+def alg8d_edge(E, N, H, s, bwd=False):
+    return (2 if bwd else 1) * (E * (2 * s * H + 8) + N * 2 * s * H)
+
+
+def alg8d_node(N, H, s, bwd=False, proj=False):
+    return (2 if bwd else 1) * N * 3 * s * H * (2 if (bwd and proj) else 1)
+
+
+def with_alg(alg, impl):
+    """(alg_bytes, flops, impl_bytes) from a §8(d) share and an implementation cost tuple."""
+    return (alg, impl[1], impl[0])
+
+
 def mask_bytes(H):
     """AGN_RELU_MASK bytes per row of one hidden layer (8 B per lane pair and dword)."""
     return 8 * max(1, (H + 63) // 64)

@@ -65,18 +65,26 @@ def mse_sum_loss(pred, y, n_global: float):
 
 
 class GradAllReduce:
-    """Flat-bucket gradient all-reduce (SUM) of a module's parameters.
+    """Bucketed gradient all-reduce (SUM) of a module's parameters, overlapped with the backward.
 
     Gradients are packed into a few contiguous buckets in the parameters' own dtype (fp32 master
-    weights: ~4 buckets for the 2.9M-parameter model, each a single RCCL ring all-reduce,
-    link-bound on xGMI) and unpacked in place. A bucket never mixes dtypes.
+    weights: ~4 buckets of <= 4 MB for the 2.9M-parameter model, each one RCCL ring all-reduce,
+    link-bound on point-to-point xGMI) and unpacked in place. A bucket never mixes dtypes.
+    Buckets are formed in REVERSE registration order, the order the backward produces them
+    (decoder, up path, ..., encoders).
+
+    `arm()` before the last (or only) micro-batch's backward: each bucket is then packed and its
+    all-reduce launched (async, on the collective stream) from a post-accumulate-grad hook the
+    moment its last gradient lands, so the transfer overlaps the rest of the backward. Calling
+    the object afterwards launches any bucket that never fired, waits for all of them and
+    unpacks. Without `arm()` everything happens in the call, after the backward.
     """
 
     def __init__(self, params, bucket_bytes=4 << 20):
         self.params = [p for p in params if p.requires_grad]
         self.buckets = []
         cur, size = [], 0
-        for p in self.params:
+        for p in reversed(self.params):
             if cur and cur[-1].dtype != p.dtype:
                 self.buckets.append(cur)
                 cur, size = [], 0
@@ -88,25 +96,64 @@ class GradAllReduce:
         if cur:
             self.buckets.append(cur)
         self._flat = None
+        self._armed = False
+        self._works = {}
+        self._pending = None
+        self._hooks = []
+        if world()[1] > 1:
+            where = {}
+            for bi, b in enumerate(self.buckets):
+                for p in b:
+                    where[id(p)] = bi
+            for p in self.params:
+                if hasattr(p, "register_post_accumulate_grad_hook"):
+                    self._hooks.append(p.register_post_accumulate_grad_hook(self._hook(where[id(p)])))
+
+    def _ensure_flat(self):
+        if self._flat is None:
+            dev = self.params[0].device
+            self._flat = [torch.empty(sum(p.numel() for p in b), dtype=b[0].dtype, device=dev)
+                          for b in self.buckets]
+
+    def arm(self):
+        if world()[1] <= 1:
+            return
+        self._armed = True
+        self._works = {}
+        self._pending = [len(b) for b in self.buckets]
+
+    def _hook(self, bi):
+        def fire(_p):
+            if not self._armed:
+                return
+            self._pending[bi] -= 1
+            if self._pending[bi] == 0:
+                self._launch(bi)
+        return fire
+
+    def _launch(self, bi):
+        self._ensure_flat()
+        flat = self._flat[bi]
+        o = 0
+        for p in self.buckets[bi]:
+            n = p.numel()
+            if p.grad is not None:
+                flat[o:o + n].copy_(p.grad.reshape(-1))
+            else:
+                flat[o:o + n].zero_()
+            o += n
+        self._works[bi] = all_reduce_(flat, async_op=True)
 
     def __call__(self):
         rank, ws = world()
         if ws <= 1:
             return
-        if self._flat is None:
-            dev = self.params[0].device
-            self._flat = [torch.empty(sum(p.numel() for p in b), dtype=b[0].dtype, device=dev)
-                          for b in self.buckets]
-        works = []
-        for b, flat in zip(self.buckets, self._flat):
-            o = 0
-            for p in b:
-                n = p.numel()
-                g = p.grad if p.grad is not None else torch.zeros_like(p)
-                flat[o:o + n].copy_(g.reshape(-1))
-                o += n
-            works.append(all_reduce_(flat, async_op=True))
-        for w, b, flat in zip(works, self.buckets, self._flat):
+        for bi in range(len(self.buckets)):
+            if bi not in self._works:
+                self._launch(bi)
+        self._armed = False
+        for bi, (b, flat) in enumerate(zip(self.buckets, self._flat)):
+            w = self._works.get(bi)
             if w is not None:
                 w.wait()
             o = 0
@@ -116,3 +163,4 @@ class GradAllReduce:
                     p.grad = torch.zeros_like(p)
                 p.grad.copy_(flat[o:o + n].view_as(p.grad))
                 o += n
+        self._works = {}

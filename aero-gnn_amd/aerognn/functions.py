@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_sum, stream)
@@ -340,12 +340,12 @@ class GMPFn(torch.autograd.Function):
             mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
                         segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
                         wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
-                        tag="proj", cost=cost_proj(N, H, sz))
+                        tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
                         resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
-                        tag="edge_fwd", cost=cost_edge_fwd(E, N, H, sz, es.nlin, train))
+                        tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin, train)))
         else:
             se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
             ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
@@ -354,7 +354,8 @@ class GMPFn(torch.autograd.Function):
                         segs=[ss, sd, se] if spec.gmp_order else [se, ss, sd],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), resid=e, out=e_out,
                         acts=ea, hpre=ehp, stats=est,
-                        tag="edge_fwd", cost=cost_edge_fwd_cat(E, N, H, x.element_size(), es.nlin, train))
+                        tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, x.element_size()),
+                                                       cost_edge_fwd_cat(E, N, H, x.element_size(), es.nlin, train)))
         agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
         kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
         mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
@@ -362,7 +363,8 @@ class GMPFn(torch.autograd.Function):
                           (kind, H, e_out.stride(0), e_out, level.rowptr, agg)],
                     wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), resid=x, out=x_out,
                     acts=na, hpre=nhp, stats=nst,
-                    tag="node_fwd", cost=cost_node_fwd(E, N, H, x.element_size(), ns.nlin, train))
+                    tag="node_fwd", cost=with_alg(alg8d_node(N, H, x.element_size()),
+                                                   cost_node_fwd(E, N, H, x.element_size(), ns.nlin, train)))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
         ctx.save_for_backward(x, e)
@@ -390,7 +392,8 @@ class GMPFn(torch.autograd.Function):
         nb_n = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=gx, gpre=gpre_n, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
                      din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n,
-                     tag="node_bwd", cost=cost_node_bwd(N, H, x.element_size(), ns.nlin))
+                     tag="node_bwd", cost=with_alg(alg8d_node(N, H, x.element_size(), bwd=True, proj=spec.trick),
+                                                   cost_node_bwd(N, H, x.element_size(), ns.nlin)))
         if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
             dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
         # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
@@ -408,7 +411,8 @@ class GMPFn(torch.autograd.Function):
         nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
                      hpre=ehp, stats=est, din=din, ln_partial=part_e, tag="edge_bwd",
-                     cost=(cost_edge_bwd if spec.trick else cost_edge_bwd_cat)(E, N, H, x.element_size(), es.nlin))
+                     cost=with_alg(alg8d_edge(E, N, H, x.element_size(), bwd=True),
+                                   (cost_edge_bwd if spec.trick else cost_edge_bwd_cat)(E, N, H, x.element_size(), es.nlin)))
         g0 = gpre_e[0]
         grads_edge = []
         if spec.trick:

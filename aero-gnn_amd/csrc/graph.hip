@@ -325,7 +325,12 @@ __global__ void row_ptr64_kernel(const int64_t* __restrict__ keys, int n, int nr
   ptr[v] = lo;
 }
 
+// Monotone float -> uint32 key with the comparison torch.argsort uses: -0.0 and +0.0 compare equal
+// (both map to +0's key, so the stable index rule decides between them), and every NaN, whatever
+// its sign bit, sorts after +inf.
 __device__ __forceinline__ uint32_t orderable(float x) {
+  if (x != x) return 0xffffffffu;
+  if (x == 0.f) x = 0.f;
   const uint32_t u = __float_as_uint(x);
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }

@@ -7,15 +7,19 @@ synthetic 1,000,000-node / 5,996,000-edge ellipsoid aero surface mesh; bf16 acti
 fp32 master weights, Adam. One step = forward (incl. the per-forward pooling hierarchy
 build, as the reference does) + MSE + backward + gradient all-reduce + Adam.
 An edge-update is one directed edge processed by one MeshGraphNetLayer (SURVEY §8d);
-EU/step is counted from the actual hierarchy (82,432,142 for C3).
+EU/step is counted from the actual hierarchy.
 
 N GPUs (torchrun): every rank trains on its own mesh of the same size (rotation seed = rank),
-one RCCL gradient all-reduce per step: weak scaling, value = total EU / max-rank time.
+one RCCL gradient all-reduce per step (bucketed, overlapped with the backward): weak scaling,
+value = total EU / max-rank time. The same run also measures the north-star scaling case,
+C4 strong scaling (BASELINE.json configs[3]: a fixed global batch of 64 ellipsoid(400,250)
+meshes split over the ranks), and reports it under "c4_strong" (disable: --no-c4).
 
---config c4 (BASELINE.json configs[3]): a fixed global batch of 64 meshes of
-ellipsoid(400,250) (rotation seed = mesh index) split contiguously over the ranks (64/N each),
-PyG-collated into micro-batches of 8 meshes with gradient accumulation, one all-reduce per step:
-strong scaling.
+--config c4 makes C4 the headline instead; --config c5 --mode fwd is the HBM stress forward.
+
+Timing: W untimed warm-up steps, then K steps with NO instrumentation, bracketed by barrier +
+synchronize, max over ranks. A separate pass of --profile-steps steps (not timed for `value`)
+records HIP events around every libaerognn launch for the per-kernel table and the roofline.
 
 Prints ONE JSON line (rank 0).
 """
@@ -24,6 +28,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
+import statistics
 import sys
 import time
 
@@ -46,6 +52,7 @@ CONFIGS = {
     "c4": (400, 250, 4, torch.bfloat16),
 }
 BATCHED = {"c4": (64, 8)}  # config: (global batch of meshes, meshes per micro-batch)
+MODEL_NAME = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
 
 
 def build_model(num_scales, dev):
@@ -70,7 +77,7 @@ def mesh_tensors(nu, nv, seed, dev, dtype):
 
 def batch_tensors(nu, nv, seeds, dev, dtype):
     """PyG-style collate (aerognn.meshgen.collate: concatenated rows, edge_index offset by the
-    running node count, `batch` = mesh index per node) of one mesh per seed, on the device."""
+    running node count, `batch` = mesh index per node), moved to the device."""
     from aerognn.meshgen import collate, ellipsoid
     b = collate([ellipsoid(nu, nv, seed=s) for s in seeds])
     t = {k: torch.from_numpy(v).to(dev) for k, v in b.items()}
@@ -79,73 +86,183 @@ def batch_tensors(nu, nv, seeds, dev, dtype):
     return t
 
 
+def level_sizes(model, t):
+    """(N_l, E_l) of every level of the hierarchy actually built for this input."""
+    level, pools = model._hierarchy(t["edge_index"], t.get("batch"), t["pos"], t["x"].shape[0])
+    return [level.N] + [p.coarse.N for p in pools], [level.E] + [p.coarse.E for p in pools]
+
+
+def layer_levels(model):
+    """Level index of every processor layer, in execution order (bsms_mgn.py:126-215)."""
+    nd = len(model.down_layers)
+    lv = []
+    for s in range(nd):
+        lv += [s] * len(model.down_layers[s])
+    lv += [nd] * len(model.bottleneck_layers)
+    for s in range(nd):
+        lv += [nd - 1 - s] * len(model.up_layers[s])
+    return lv
+
+
 def edge_updates(model, t):
     """EU per step = sum over processor layers of the edge count of the level it runs on."""
-    level, pools = model._hierarchy(t["edge_index"], t.get("batch"), t["pos"], t["x"].shape[0])
-    E = [level.E] + [p.coarse.E for p in pools]
-    nd = len(model.down_layers)
-    eu = sum(len(model.down_layers[s]) * E[s] for s in range(nd))
-    eu += len(model.bottleneck_layers) * E[nd]
-    eu += sum(len(model.up_layers[s]) * E[nd - 1 - s] for s in range(nd))
-    return eu, E
+    _, E = level_sizes(model, t)
+    return sum(E[l] for l in layer_levels(model)), E
 
 
-def cpu_baseline(num_scales, seconds_hint=20.0):
-    """Oracle (oracle/refcpu.py, op-for-op the reference's CPU path) timed on host cores:
-    one fp32 training step (fwd + MSE + bwd) of the same model on a bounded sample mesh."""
+def alg_step_cost(model, t, s, train, H=128, d_n=6, d_e=4, d_out=4):
+    """SURVEY §8(d) algorithmic minimum of one step (fully fused): (bytes, flops).
+
+    Per processor layer on level l: B = E(2sH + 8) + N(8sH), F = 8H^2 E + 14H^2 N.
+    Pool l -> l+1: sH(N_l + E_l + N_l+1 + E_l+1) + 24 E_l + 12 N_l; unpool: sH(N_l+1 + 2 N_l) + 4 N_l.
+    Encoders/decoder: read input + write latent; flops exact. Training = 3x forward."""
+    N, E = level_sizes(model, t)
+    B = F = 0.0
+    for l in layer_levels(model):
+        B += E[l] * (2 * s * H + 8) + N[l] * 8 * s * H
+        F += 8 * H * H * E[l] + 14 * H * H * N[l]
+    for l in range(len(N) - 1):
+        B += s * H * (N[l] + E[l] + N[l + 1] + E[l + 1]) + 24 * E[l] + 12 * N[l]
+        B += s * H * (N[l + 1] + 2 * N[l]) + 4 * N[l]
+    B += N[0] * (d_n * s + s * H) + E[0] * (d_e * s + s * H) + N[0] * (s * H + d_out * s)
+    F += E[0] * 2 * (d_e * H + 3 * H * H) + N[0] * 2 * (d_n * H + 3 * H * H) + N[0] * 2 * (3 * H * H + H * d_out)
+    k = 3.0 if train else 1.0
+    return k * B, k * F
+
+
+def cpu_info():
+    name = platform.processor() or "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                name = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return name
+
+
+def _median_time(fn, reps=3):
+    fn()  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def cpu_baseline(num_scales, nu=250, nv=200):
+    """The oracle (oracle/refcpu.py: the reference's aten ops in order, verified bitwise-equal to
+    the imported reference in tools/make_goldens.py) timed on this box's host cores, BASELINE.md
+    §3 protocol (1 warm-up, median of 3), fp32, on a bounded sample of the headline model: the
+    same BSMS model's forward on a 50,000-node / 299,000-edge ellipsoid (~20 s of CPU work)."""
     from aerognn.meshgen import ellipsoid
     from oracle import refcpu as R
     nthreads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(nthreads)
-    nu, nv = 250, 200  # 50,000 nodes / 299,000 edges
     m = ellipsoid(nu, nv, seed=0)
     t = {k: torch.from_numpy(v) for k, v in m.items()}
     model, kw = build_model(num_scales, "cpu")
-    p = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    p = {k: v.detach().clone() for k, v in model.state_dict().items()}
     cfg = R.cfg_from_kwargs(**kw)
     batch = torch.zeros(t["x"].shape[0], dtype=torch.long)
-    # EU of the sample
     down, bott, up = R.bsms_schedule(cfg["processor_size"], cfg["num_scales"], cfg["layers_per_scale"])
-    Es, ei, pos, b = [], t["edge_index"], t["pos"], batch
-    Es.append(ei.shape[1])
+    Es, ei, pos, b = [t["edge_index"].shape[1]], t["edge_index"], t["pos"], batch
     node = torch.zeros(t["x"].shape[0], 1)
     for _ in down:
         node, _e, ei, b, pos, _a = R.downsample(node, torch.zeros(ei.shape[1], 1), ei, b, pos, cfg["stride"], True)
         Es.append(ei.shape[1])
     eu = sum(c * Es[i] for i, c in enumerate(down)) + bott * Es[len(down)] + \
         sum(c * Es[len(down) - 1 - i] for i, c in enumerate(up))
-    t0 = time.perf_counter()
-    pred = R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch, t["pos"], stable=True)
-    loss = torch.nn.functional.mse_loss(pred, t["y"])
-    loss.backward()
-    dt = time.perf_counter() - t0
+
+    def fwd():
+        with torch.no_grad():
+            R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch, t["pos"], stable=True)
+    dt = _median_time(fwd)
     return {"value": eu / dt / 1e6, "unit": "M edge-updates/s", "cores": nthreads, "kind": "port",
-            "sample": f"1 fp32 train step (fwd+MSE+bwd) of the same BSMS-{num_scales} model, oracle/refcpu.py "
-                      f"(the reference's aten ops in order) on a {nu * nv}-node/{m['edge_index'].shape[1]}-edge "
-                      f"ellipsoid, {eu} EU, {dt:.1f} s, torch threads={nthreads}"}
+            "cpu": cpu_info(), "torch": torch.__version__, "dtype": "f32",
+            "sample": f"fp32 forward (no_grad) of the same BSMS-{num_scales} model, oracle/refcpu.py, on a "
+                      f"{nu * nv}-node/{m['edge_index'].shape[1]}-edge ellipsoid ({eu} EU); 1 warm-up, median of 3 "
+                      f"= {dt:.2f} s; torch threads={nthreads}. Full BASELINE.md §3 plan (C1-C3 fwd, C1/C2 train): "
+                      f"bench.py --cpu-plan, committed as profiles/r2_cpu_plan.json"}
 
 
-def setup_bsms_gnn(nu, nv, seed, dev, dtype, num_levels=3):
-    """The stale BSMS-GNN design (BSMS_MeshGraphNet) on the same mesh: the BFS
-    bi-stride hierarchy is built once per mesh (MultiScaleGraphPreprocessor, 'done once during
-    data loading'), timed separately and reported as preprocess_ms."""
-    from models.bsms_mgn import BSMS_MeshGraphNet, MultiScaleGraphPreprocessor
-    t = mesh_tensors(nu, nv, seed=seed, dev=dev, dtype=dtype)
+def cpu_plan():
+    """BASELINE.md §3 in full: forward at C1/C2/C3 and train step at C1/C2, 1 warm-up + median
+    of 3, fp32, oracle/refcpu.py on host cores (minutes of CPU work; run once, results committed)."""
+    from aerognn.meshgen import ellipsoid
+    from oracle import refcpu as R
+    nthreads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(nthreads)
+    out = {"cpu": cpu_info(), "cores": nthreads, "torch": torch.__version__, "dtype": "f32",
+           "protocol": "1 warm-up, median of 3", "rows": []}
+    for name, (nu, nv), S, modes in (("C1", (40, 25), 1, ("fwd", "train")), ("C2", (400, 250), 1, ("fwd", "train")),
+                                     ("C3", (1000, 1000), 4, ("fwd",))):
+        m = ellipsoid(nu, nv, seed=0)
+        t = {k: torch.from_numpy(v) for k, v in m.items()}
+        model, kw = build_model(S, "cpu")
+        cfg = R.cfg_from_kwargs(**kw)
+        batch = torch.zeros(t["x"].shape[0], dtype=torch.long)
+        if S == 1:
+            eu = 15 * t["edge_index"].shape[1]
+            run = lambda p: R.mgn_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg)  # noqa: E731
+        else:
+            eu = None
+            run = lambda p: R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch,  # noqa: E731
+                                           t["pos"], stable=True)
+        if eu is None:
+            down, bott, up = R.bsms_schedule(cfg["processor_size"], cfg["num_scales"], cfg["layers_per_scale"])
+            Es, ei, pos, b = [t["edge_index"].shape[1]], t["edge_index"], t["pos"], batch
+            node = torch.zeros(t["x"].shape[0], 1)
+            for _ in down:
+                node, _e, ei, b, pos, _a = R.downsample(node, torch.zeros(ei.shape[1], 1), ei, b, pos, 2, True)
+                Es.append(ei.shape[1])
+            eu = sum(c * Es[i] for i, c in enumerate(down)) + bott * Es[len(down)] + \
+                sum(c * Es[len(down) - 1 - i] for i, c in enumerate(up))
+        p0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+        for mode in modes:
+            if mode == "fwd":
+                def fn():
+                    with torch.no_grad():
+                        run(p0)
+            else:
+                pt = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+                opt = torch.optim.Adam(list(pt.values()), lr=1e-3)
 
-    class _D:
-        pass
-    d = _D()
-    d.edge_index, d.pos, d.num_nodes = t["edge_index"], t["pos"], t["x"].shape[0]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    multi = MultiScaleGraphPreprocessor(num_levels).create_multiscale_graph(d)
-    torch.cuda.synchronize()
-    prep_ms = 1e3 * (time.perf_counter() - t0)
-    torch.manual_seed(0)
-    model = BSMS_MeshGraphNet(6, 4, 4, num_levels=num_levels, latent_dim=128, hidden_dim=128, pos_dim=3).to(dev)
-    Es = [int(ei.shape[1]) for ei in multi["edge_indices"]]
-    eu = sum(Es)  # one GMP per level on the way down (levels 0..L-1) + the bottom GMP (level L)
-    return model, t, multi, eu, Es, prep_ms
+                def fn():
+                    torch.nn.functional.mse_loss(run(pt), t["y"]).backward()
+                    opt.step()
+                    opt.zero_grad(set_to_none=True)
+            dt = _median_time(fn)
+            out["rows"].append({"config": name, "mode": mode, "nodes": int(t["x"].shape[0]),
+                                "edges": int(t["edge_index"].shape[1]), "eu": int(eu), "seconds": dt,
+                                "M_EU_per_s": eu / dt / 1e6})
+            print(json.dumps(out["rows"][-1]), flush=True)
+    return out
+
+
+def kernel_table(prof, steps, elapsed_step_s):
+    agg = {}
+    for tag, cost, s, e in prof:
+        ms = s.elapsed_time(e)
+        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0, 0.0, False])
+        a[0] += 1
+        a[1] += ms
+        if cost:
+            a[2] += cost[0]
+            a[3] += cost[1]
+            a[4] += cost[2] if len(cost) > 2 else cost[0]
+            a[5] = True
+    tab = {}
+    for tag, (n, ms, by, fl, impl, has) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        sec = ms * 1e-3
+        tab[tag] = {"launches_per_step": n / steps, "avg_us": 1e3 * ms / n, "ms_per_step": ms / steps,
+                    "share_of_step": (ms / steps) / (1e3 * elapsed_step_s),
+                    "alg_GBs": (by / sec / 1e9) if has else None, "impl_GBs": (impl / sec / 1e9) if has else None,
+                    "alg_TFLOPs": (fl / sec / 1e12) if has else None,
+                    "_sum": (n, ms, by, fl, impl, has)}
+    return tab
 
 
 def main():
@@ -157,11 +274,16 @@ def main():
     ap.add_argument("--mode", default="train", choices=["train", "fwd"])
     ap.add_argument("--model", default="bsms_mgn", choices=["bsms_mgn", "bsms_gnn"],
                     help="bsms_mgn: BiStridedMeshGraphNet (the headline); bsms_gnn: the stale BSMS_MeshGraphNet")
+    ap.add_argument("--profile-steps", type=int, default=1, help="extra instrumented steps for the kernel table")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                                      "r1e_pmc_traffic.json"),
+    ap.add_argument("--no-c4", action="store_true", help="skip the secondary C4 strong-scaling measurement")
+    ap.add_argument("--cpu-plan", action="store_true", help="run BASELINE.md §3's full CPU plan and exit")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"),
                     help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels")
     args = ap.parse_args()
+    if args.cpu_plan:
+        print(json.dumps(cpu_plan()))
+        return
 
     from aerognn import core, dist as D
     rank, ws = D.init_from_env()
@@ -170,117 +292,154 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     nu, nv, S, dtype = CONFIGS[args.config]
-
-    extra = {}
-    scaling = "weak"
-    if args.model == "bsms_mgn" and args.config in BATCHED:
-        gb, mb = BATCHED[args.config]
-        if gb % ws:
-            raise SystemExit(f"bench: global batch {gb} is not divisible by {ws} ranks")
-        per = gb // ws
-        seeds = list(range(rank * per, (rank + 1) * per))
-        model, kw = build_model(S, dev)
-        batches = [batch_tensors(nu, nv, seeds[i:i + mb], dev, dtype) for i in range(0, per, mb)]
-        eus = [edge_updates(model, b) for b in batches]
-        eu_step = sum(e for e, _ in eus)
-        Es = eus[0][1]
-        scaling = "strong"
-        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
-        workload = (f"BSMS-MGN {S}-scale U-Net {what}, global batch {gb} meshes of {nu * nv} nodes / "
-                    f"{batches[0]['edge_index'].shape[1] // min(mb, per)} edges, {per} per GPU in micro-batches "
-                    f"of {min(mb, per)} (gradient accumulation)")
-        model_name = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
-        extra["global_batch_meshes"] = gb
-    elif args.model == "bsms_mgn":
-        model, kw = build_model(S, dev)
-        t = mesh_tensors(nu, nv, seed=rank, dev=dev, dtype=dtype)
-        batches = [t]
-        eu_step, Es = edge_updates(model, t)
-        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
-        workload = (f"BSMS-MGN {S}-scale U-Net {what}, "
-                    f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU")
-        model_name = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
-    else:
-        model, t, multi, eu_step, Es, prep_ms = setup_bsms_gnn(nu, nv, rank, dev, dtype)
-        batches = [t]
-        extra["preprocess_ms"] = round(prep_ms, 1)
-        what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
-        workload = (f"BSMS-GNN (stale design) 3-level {what}, "
-                    f"{t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} edges per GPU, BFS hierarchy prebuilt")
-        model_name = "BSMS_MeshGraphNet(num_levels=3, latent=128, hidden=128, WeightedEdgeConv pooling)"
-
-    def fwd(b):
-        if args.model == "bsms_mgn":
-            return model(b["x"], b["edge_attr"], b["edge_index"], batch=b.get("batch"), pos=b["pos"])
-        return model(b["x"], b["edge_attr"], b["edge_index"], multi_data=multi)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
-    allreduce = D.GradAllReduce(model.parameters())
-    n_glob = D.global_count(sum(b["y"].numel() for b in batches), dev)
-
-    def step():
-        if args.mode == "train":
-            for b in batches:  # gradient accumulation over micro-batches (sum loss / global count)
-                loss = D.mse_sum_loss(fwd(b), b["y"], n_glob)
-                loss.backward()
-            allreduce()
-            opt.step()
-            opt.zero_grad(set_to_none=True)
-        else:
-            with torch.no_grad():
-                for b in batches:
-                    fwd(b)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    core.PROF = []
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if ws > 1:
-        torch.distributed.barrier()
-    elapsed = time.perf_counter() - t0
-    prof, core.PROF = core.PROF, None
-    if ws > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        if D._host_staged():
-            e = e.cpu()
-        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(e.item())
-
-    # per-kernel device time from the HIP events recorded on the launch stream
-    agg = {}
-    for tag, cost, s, e in prof:
-        ms = s.elapsed_time(e)
-        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0])
-        a[0] += 1
-        a[1] += ms
-        a[2] += cost[0] if cost else 0.0
-        a[3] += cost[1] if cost else 0.0
-    dom = max(agg.items(), key=lambda kv: kv[1][1]) if agg else None
-    roof = None
-    kernels = {}
-    for tag, (n, ms, by, fl) in agg.items():
-        kernels[tag] = {"launches": n, "avg_us": 1e3 * ms / n, "alg_GBs": by / (ms * 1e-3) / 1e9,
-                        "alg_TFLOPs": fl / (ms * 1e-3) / 1e12, "share_of_step": ms / (1e3 * elapsed)}
     dname = "bf16" if dtype == torch.bfloat16 else "f32"
-    if dom:
-        tag, (n, ms, by, fl) = dom
-        ach = by / n / (ms / n * 1e-3) / 1e9
-        traffic = None
-        if (args.traffic and os.path.exists(args.traffic) and args.config == "c3" and args.mode == "train"
-                and args.model == "bsms_mgn"):
-            traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(tag)
-        roof = {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "alg_bytes_per_launch": by / n, "avg_launch_us": 1e3 * ms / n,
-                "mfma_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "mfma_peak": MFMA_PEAK[dname]}
+    s_el = 2 if dtype == torch.bfloat16 else 4
+    what = "train step (fwd+MSE+bwd+allreduce+Adam)" if args.mode == "train" else "forward (no_grad)"
 
+    def setup(config):
+        """(model, batches, eu_step, level_edges, workload, scaling, extra) for one config."""
+        nu, nv, S, _ = CONFIGS[config]
+        extra = {}
+        if args.model == "bsms_mgn" and config in BATCHED:
+            gb, mb = BATCHED[config]
+            if gb % ws:
+                raise SystemExit(f"bench: global batch {gb} is not divisible by {ws} ranks")
+            per = gb // ws
+            seeds = list(range(rank * per, (rank + 1) * per))
+            model, _ = build_model(S, dev)
+            batches = [batch_tensors(nu, nv, seeds[i:i + mb], dev, dtype) for i in range(0, per, mb)]
+            eus = [edge_updates(model, b) for b in batches]
+            workload = (f"BSMS-MGN {S}-scale U-Net {what}, global batch {gb} meshes of {nu * nv} nodes / "
+                        f"{batches[0]['edge_index'].shape[1] // min(mb, per)} edges, {per} per GPU in micro-batches "
+                        f"of {min(mb, per)} (gradient accumulation)")
+            extra["global_batch_meshes"] = gb
+            return model, batches, sum(e for e, _ in eus), eus[0][1], workload, "strong", extra
+        if args.model == "bsms_mgn":
+            model, _ = build_model(S, dev)
+            t = mesh_tensors(nu, nv, seed=rank, dev=dev, dtype=dtype)
+            eu, Es = edge_updates(model, t)
+            workload = (f"BSMS-MGN {S}-scale U-Net {what}, {t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} "
+                        f"edges per GPU")
+            return model, [t], eu, Es, workload, "weak", extra
+        from models.bsms_mgn import BSMS_MeshGraphNet, MultiScaleGraphPreprocessor
+        t = mesh_tensors(nu, nv, seed=rank, dev=dev, dtype=dtype)
+        d = type("D", (), {})()
+        d.edge_index, d.pos, d.num_nodes = t["edge_index"], t["pos"], t["x"].shape[0]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        multi = MultiScaleGraphPreprocessor(3).create_multiscale_graph(d)
+        torch.cuda.synchronize()
+        extra["preprocess_ms"] = round(1e3 * (time.perf_counter() - t0), 1)
+        extra["multi"] = multi
+        torch.manual_seed(0)
+        model = BSMS_MeshGraphNet(6, 4, 4, num_levels=3, latent_dim=128, hidden_dim=128, pos_dim=3).to(dev)
+        Es = [int(ei.shape[1]) for ei in multi["edge_indices"]]
+        workload = (f"BSMS-GNN (stale design) 3-level {what}, {t['x'].shape[0]} nodes / {t['edge_index'].shape[1]} "
+                    f"edges per GPU, BFS hierarchy prebuilt")
+        return model, [t], sum(Es), Es, workload, "weak", extra
+
+    def make_step(model, batches, extra):
+        multi = extra.pop("multi", None)
+
+        def fwd(b):
+            if multi is None:
+                return model(b["x"], b["edge_attr"], b["edge_index"], batch=b.get("batch"), pos=b["pos"])
+            return model(b["x"], b["edge_attr"], b["edge_index"], multi_data=multi)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        allreduce = D.GradAllReduce(model.parameters())
+        n_glob = D.global_count(sum(b["y"].numel() for b in batches), dev)
+
+        def step():
+            if args.mode == "train":
+                for i, b in enumerate(batches):  # gradient accumulation over micro-batches
+                    if i == len(batches) - 1:
+                        allreduce.arm()  # buckets all-reduce as their grads land (overlaps the backward)
+                    D.mse_sum_loss(fwd(b), b["y"], n_glob).backward()
+                allreduce()
+                opt.step()
+                opt.zero_grad(set_to_none=True)
+            else:
+                with torch.no_grad():
+                    for b in batches:
+                        fwd(b)
+        return step
+
+    def timed_run(step, steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if ws > 1:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        if ws > 1:
+            e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            if D._host_staged():
+                e = e.cpu()
+            torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+            elapsed = float(e.item())
+        return elapsed
+
+    model, batches, eu_step, Es, workload, scaling, extra = setup(args.config)
+    step = make_step(model, batches, extra)
+    elapsed = timed_run(step, args.steps, args.warmup)
+    step_s = elapsed / args.steps
     value = eu_step * args.steps * ws / elapsed / 1e6
+
+    # instrumented pass (not part of `value`): HIP events around every libaerognn launch
+    kernels, roof = {}, None
+    if args.profile_steps > 0:
+        core.PROF = []
+        torch.cuda.synchronize()
+        for _ in range(args.profile_steps):
+            step()
+        torch.cuda.synchronize()
+        prof, core.PROF = core.PROF, None
+        kernels = kernel_table(prof, args.profile_steps, step_s)
+    if args.model == "bsms_mgn":
+        B, F = 0.0, 0.0
+        for b in batches:
+            bb, ff = alg_step_cost(model, b, s_el, args.mode == "train")
+            B, F = B + bb, F + ff
+        t_hbm, t_mfma = B / (HBM_PEAK_GBS * 1e9), F / (MFMA_PEAK[dname] * 1e12)
+        t_roof = max(t_hbm, t_mfma)
+        step_roof = {"alg_bytes": B, "alg_flops": F, "t_roof_ms": 1e3 * t_roof, "t_measured_ms": 1e3 * step_s,
+                     "bound": "hbm" if t_hbm >= t_mfma else "mfma", "frac": t_roof / step_s,
+                     "achieved_GBs": B / step_s / 1e9, "achieved_TFLOPs": F / step_s / 1e12,
+                     "basis": "SURVEY §8(d) fully-fused minimum: per layer E(2sH+8)+N(8sH) bytes, 8H^2E+14H^2N "
+                              "flops, + pool/unpool/encoders/decoder; x3 for training"}
+    else:
+        step_roof = None
+    if kernels:
+        tag, kt = next(iter(kernels.items()))  # most device time over ALL recorded launches
+        n, ms, by, fl, impl, has = kt["_sum"]
+        traffic = None
+        if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and args.mode == "train" \
+                and args.model == "bsms_mgn":
+            traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(tag)
+        basis_bytes = by if has else None
+        ach = basis_bytes / n / (ms / n * 1e-3) / 1e9 if basis_bytes else None
+        roof = {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic,
+                "alg_bytes_per_launch": basis_bytes / n if basis_bytes else None,
+                "traffic_over_alg": (traffic / (basis_bytes / n)) if (traffic and basis_bytes) else None,
+                "avg_launch_us": 1e3 * ms / n, "launches_per_step": n / args.profile_steps,
+                "mfma_tflops": round(fl / (ms * 1e-3) / 1e12, 2) if has else None, "mfma_peak": MFMA_PEAK[dname],
+                "alg_basis": "SURVEY §8(d) share of the fused layer (DESIGN.md §5)" if has else
+                             "none: this kernel is outside the §8(d) fused minimum",
+                "step": step_roof}
+        for v in kernels.values():
+            v.pop("_sum")
+    elif step_roof:
+        roof = {"kernel": None, "bound": step_roof["bound"], "achieved": step_roof["achieved_GBs"],
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_roof["frac"], "traffic": None, "step": step_roof}
+
     out = {
         "metric": "million edge-updates/sec, 1M-node/6M-edge mesh, 1->8 MI355X",
         "value": round(value, 2),
@@ -288,18 +447,30 @@ def main():
         "n_gpus": ws,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "ms_per_step": round(1e3 * step_s, 3),
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": dname,
         "data": "synthetic ellipsoid aero surface mesh (aerognn.meshgen), random-init weights (seed 0)",
-        "config": {"workload": workload, "model": model_name, **extra,
-                   "mode": args.mode, "edge_updates_per_step_per_gpu": eu_step, "level_edges": Es,
+        "config": {"workload": workload, "model": MODEL_NAME if args.model == "bsms_mgn" else "BSMS_MeshGraphNet",
+                   **{k: v for k, v in extra.items() if k != "multi"}, "mode": args.mode,
+                   "edge_updates_per_step_per_gpu": eu_step, "level_edges": Es,
                    "global_batch": extra.get("global_batch_meshes", ws), "parallelism": f"dp{ws}"},
         "roofline": roof,
         "kernels": kernels,
     }
+    if args.model == "bsms_mgn" and args.config == "c3" and args.mode == "train" and not args.no_c4:
+        del model, batches, step
+        torch.cuda.empty_cache()
+        m4, b4, eu4, _, wl4, _, ex4 = setup("c4")
+        st4 = make_step(m4, b4, ex4)
+        k4 = min(args.steps, 5)
+        el4 = timed_run(st4, k4, 1)
+        out["c4_strong"] = {"value": round(eu4 * k4 * ws / el4 / 1e6, 2), "unit": "M edge-updates/s",
+                            "ms_per_step": round(1e3 * el4 / k4, 3), "steps": k4, "warmup": 1, "scaling": "strong",
+                            "workload": wl4, "edge_updates_per_step_per_gpu": eu4,
+                            "note": "BASELINE.json configs[3] / north_star's 1->8 scaling case (fixed global batch)"}
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.model == "bsms_mgn":
         out["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:

@@ -46,7 +46,7 @@ def _mesh(nu, nv, seed):
     return {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in m.items()}
 
 
-def _worker(rank, ws, port, out):
+def _worker(rank, ws, port, out, overlap):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -65,19 +65,25 @@ def _worker(rank, ws, port, out):
     pred = R.bsms_forward(params, t["x"].double(), t["edge_attr"].double(), t["edge_index"], cfg, batch,
                           t["pos"].double(), stable=True)
     loss = D.mse_sum_loss(pred, t["y"].double(), n_glob)
+    ar = D.GradAllReduce(params.values(), bucket_bytes=16 << 10)  # several buckets
+    if overlap:  # buckets launch from post-accumulate-grad hooks during the backward
+        ar.arm()
     loss.backward()
-    D.GradAllReduce(params.values())()
+    if overlap:
+        assert len(ar._works) == len(ar.buckets)  # every bucket fired inside the backward
+    ar()
     if rank == 0:
         torch.save({k: v.grad for k, v in params.items()}, out)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_gradients_equal_union_batch(tmp_path):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_gradients_equal_union_batch(tmp_path, overlap):
     from aerognn.meshgen import collate, ellipsoid
     from oracle import refcpu as R
     out = str(tmp_path / "g.pt")
-    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), out, overlap), nprocs=2, join=True, start_method="spawn")
     g_dp = torch.load(out, weights_only=True)
 
     params, cfg = _setup()

@@ -124,8 +124,9 @@ def test_c2_layer_fp32_vs_oracle():
         xo, eo = layer(x.to(DEV), e.to(DEV), ei)
     for got, ref in ((xo, xr), (eo, er)):
         got = got.cpu()
-        assert rel_l2(got, ref) <= 1e-5
-        assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) * 10
+        r, m = rel_l2(got, ref), float((got - ref).abs().max()) / float(ref.abs().max())
+        print(f"C2 layer: rel-L2 {r:.2e}, max-elem {m:.2e}")
+        assert r <= 1e-5 and m <= 1e-5
 
 
 def test_c3_pooling_maps_bitexact_vs_oracle():
@@ -139,11 +140,13 @@ def test_c3_pooling_maps_bitexact_vs_oracle():
     batch = torch.zeros(N, dtype=torch.long)
     ref1 = R.downsample(node, edge, m["edge_index"], batch, m["pos"], 2, stable=True)
     ref2 = R.downsample(ref1[0], ref1[1], ref1[2], ref1[3], ref1[4], 2, stable=True)
+    ref3 = R.downsample(ref2[0], ref2[1], ref2[2], ref2[3], ref2[4], 2, stable=True)  # all 3 C3 levels
     model = BiStridedMeshGraphNet(6, 4, 4, hidden_dim_processor=8, stride=2).to(DEV)
     got1 = model._downsample(node.to(DEV), edge.to(DEV), m["edge_index"].to(DEV), batch.to(DEV),
                              m["pos"].to(DEV))
     got2 = model._downsample(*[t for t in got1[:5]])
-    for got, ref in ((got1, ref1), (got2, ref2)):
+    got3 = model._downsample(*[t for t in got2[:5]])
+    for got, ref in ((got1, ref1), (got2, ref2), (got3, ref3)):
         cn, ce, cei, cb, cp, f2c = [t.cpu() for t in got]
         assert torch.equal(f2c, ref[5])
         assert torch.equal(cei, ref[2])

@@ -26,10 +26,12 @@ def _lib_loaded():
 
 
 def _fwd_ok(got, ref, tol=FWD):
+    """SURVEY §8 fp32 bar, both parts: rel-L2 <= tol and max|err| <= tol * max|ref|."""
     got = got.detach().float().cpu()
     ref = ref.float()
     r, m = rel_l2(got, ref), max_rel(got, ref)
-    assert r <= tol and m <= 10 * tol, (r, m)
+    print(f"fwd rel-L2 {r:.2e}, max-elem {m:.2e} (of max|ref|)")
+    assert r <= tol and m <= tol, (r, m)
 
 
 def _load(model, d):

@@ -15,7 +15,9 @@ import os
 import sys
 
 # bench.py tag -> kernel-name prefix of the launch it times (bf16 H=128 C3 workload)
-TAGS = {"edge_bwd": "mlp_bwd_res_kernel", "edge_fwd": "mlp_fwd_res_kernel"}
+TAGS = {"edge_bwd": "mlp_bwd_res_kernel", "edge_fwd": "mlp_fwd_res_kernel", "wgrad": "wgrad_kernel",
+        "segment_sum": "segment_sum_kernel", "gather_rows": "gather_rows_kernel",
+        "edge_bwd_fused": "edge_bwd_fused_kernel"}
 
 
 def _rows(d):

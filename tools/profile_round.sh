@@ -3,17 +3,22 @@
 #   1. rocprofv3 --kernel-trace --stats of bench.py (C3)         -> gpurun_out/prof_$TAG
 #   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), kernel trace only -> gpurun_out/pmc_{fetch,write}_$TAG
 #   3. tools/pmc_traffic.py -> gpurun_out/pmc_traffic_$TAG.json
+#   4. one MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE) -> mfma_$TAG.json
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -e
-TAG=${1:-r1}
+TAG=${1:-r2}
 STEPS=${2:-3}
 R=$PWD
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$R"
+B="bench.py --no-cpu-baseline --no-c4"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o c3 -- \
-    python bench.py --steps $STEPS --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1
+    python $B --steps $STEPS --warmup 1 > gpurun_out/prof_$TAG.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$TAG -o c3 -- \
-    python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch_$TAG.log 2>&1
+    python $B --steps 1 --warmup 1 > gpurun_out/pmc_fetch_$TAG.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o c3 -- \
-    python bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_write_$TAG.log 2>&1
+    python $B --steps 1 --warmup 1 > gpurun_out/pmc_write_$TAG.log 2>&1
 python tools/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_traffic_$TAG.json
+timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
+    -d gpurun_out/pmc_mfma_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_mfma_$TAG.log 2>&1
+python tools/mfma_busy.py gpurun_out/pmc_mfma_$TAG gpurun_out/mfma_$TAG.json
