@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libaerognn.so")
+# AEROGNN_LIB: an alternative build of the same library (A/B measurements only)
+LIB_PATH = os.environ.get("AEROGNN_LIB") or os.path.join(_HERE, "libaerognn.so")
 
 MAX_LIN = 8
 MAX_SEG = 3
@@ -74,6 +75,12 @@ class WecArgs(C.Structure):
                 ("dpa", vp), ("dpb", vp), ("dtx", vp), ("dw_in", vp), ("partial", vp)]
 
 
+class EdgeBwdArgs(C.Structure):
+    _fields_ = [("rows", i32), ("nblk", i32), ("wtpk", vp * 4), ("g", vp), ("g2", vp), ("gidx", vp), ("g3", vp),
+                ("act", vp * 3), ("mask", vp * 3), ("de", vp), ("g0", vp), ("dw_partial", vp), ("db_partial", vp),
+                ("stamps", vp)]
+
+
 class PackDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
                 ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
@@ -92,7 +99,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_collate",
-            "agn_global_pool", "agn_mlp_bwd_fused")
+            "agn_global_pool", "agn_edge_bwd_fused", "agn_wgrad_reduce")
 
 
 class AeroGNNError(RuntimeError):
@@ -176,6 +183,9 @@ def lib():
             "agn_subgraph_edges": (i32, [vp, vp, i32, vp, vp, vp, C.POINTER(i32), vp, vp]),
             "agn_scatter_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
             "agn_wec_blocks": (i32, [i32]),
+            "agn_edge_bwd_blocks": (i32, [i32]),
+            "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
+            "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_wec_forward": (i32, [C.POINTER(WecArgs), vp]),
             "agn_wec_backward": (i32, [C.POINTER(WecArgs), vp]),
         }

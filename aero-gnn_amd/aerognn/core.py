@@ -253,6 +253,52 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
     return a.ln_rows
 
 
+STAMPS = None  # diagnostics: a uint64 device tensor of 2*4*8*32 entries -> agn_edge_bwd_fused phase clocks
+
+
+def fused_edge_bwd_ok(rows, dtype, hidden, nlin, has_ln, acts, hpre):
+    """agn_edge_bwd_fused applies: bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN) large
+    enough for the persistent kernels, saves in the AGN_TILED layout. Opt-in (AEROGNN_FUSED_EDGE_BWD=1):
+    it is exact (tests/test_gpu_fullsize.py) but measured slower than the split path
+    (agn_mlp_backward + agn_wgrad) at C3 — DESIGN.md §9 has the phase clocks."""
+    import os
+    return (os.environ.get("AEROGNN_FUSED_EDGE_BWD", "0") == "1" and dtype == torch.bfloat16 and hidden == 128
+            and nlin == 4 and has_ln and rows >= 64 * 1024 and hpre is not None and is_tiled(hpre)
+            and len(acts) == 3 and all(is_tiled(t) and _mask_of(t) is not None for t in acts))
+
+
+def edge_bwd_fused(*, rows, wtpk, g, g2, gidx, g3, acts, de, g0, tag=None, cost=None):
+    """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32) after the
+    fixed-order slab reduction (agn_wgrad_reduce)."""
+    lib = L.lib()
+    dev = g3.device
+    H = 128
+    nblk = int(lib.agn_edge_bwd_blocks(int(rows)))
+    dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
+    dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
+    a = L.EdgeBwdArgs()
+    a.rows, a.nblk = int(rows), nblk
+    for i in range(4):
+        a.wtpk[i] = wtpk[i]
+    a.g, a.g2, a.gidx, a.g3 = ptr(g), ptr(g2), ptr(gidx), ptr(g3)
+    for i in range(3):
+        a.act[i] = ptr(acts[i])
+        a.mask[i] = ptr(_mask_of(acts[i]))
+    a.de, a.g0, a.dw_partial, a.db_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp)
+    a.stamps = ptr(STAMPS)
+    with timed(tag, cost):
+        check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
+    dw = torch.empty(3, H, H, dtype=torch.float32, device=dev)
+    db = torch.empty(3, H, dtype=torch.float32, device=dev)
+    b = L.WgradBatch()
+    b.n = 3
+    for l in range(3):
+        b.d[l] = L.WgradDesc(None, None, H, H, H, H, int(rows), H, ptr(dwp[l * nblk * H * H:]), ptr(dbp[l * nblk * H:]),
+                             ptr(dw[l]), ptr(db[l]), 0, 0)
+    check(lib.agn_wgrad_reduce(C.byref(b), nblk, stream()), "wgrad_reduce")
+    return dw, db
+
+
 def reduce_partials(partial, nw, n, out):
     check(L.lib().agn_reduce_partials(ptr(partial), nw, n, ptr(out), stream()), "reduce_partials")
 

@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_bwd_ok, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_sum, stream)
@@ -397,23 +397,40 @@ class GMPFn(torch.autograd.Function):
         if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
             dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
         # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
-        gpre_e = _alloc_gpre(es, E, dt, dev, rowmajor=(0,) if spec.trick else ())  # trick: dP_s/dP_d sums read g0
+        fused = spec.trick and es.ln is not None and fused_edge_bwd_ok(E, dt, H, es.nlin, True, ea or [], ehp)
         nb_e = bwd_nblocks(E)
         part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
         de = torch.empty_like(e)
-        if spec.trick:
-            din = [(H, de, True)]
+        sz = x.element_size()
+        if fused:
+            # LayerNorm backward alone (G3, LN parameter partials), then the fused chain + dW kernel
+            g3 = tiled_empty(E, H, dt, dev)
+            nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=1, out_dim=H, in_dim=H, wtpk=[es.wtpk()[-1]],
+                                acts=[], g=ge, g2=dagg, gidx=lv.dst, gpre=[g3], ln_g=es.lnp()[0], hpre=ehp,
+                                stats=est, din=[], ln_partial=part_e, tag="edge_ln_bwd",
+                                cost=with_alg(0, (E * (3 * H * sz + 12) + N * H * sz, 0)))
+            g0 = torch.empty(E, H, dtype=dt, device=dev)
+            dW13, db13 = edge_bwd_fused(rows=E, wtpk=es.wtpk(), g=ge, g2=dagg, gidx=lv.dst, g3=g3, acts=ea, de=de,
+                                        g0=g0, tag="edge_bwd",
+                                        cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True),
+                                                      (E * (H * sz * 7 + 24 + 4) + N * H * sz, 2 * E * H * H * 7)))
         else:
-            dxs = torch.empty(E, H, dtype=dt, device=dev)
-            dxd = torch.empty(E, H, dtype=dt, device=dev)
-            din = [(H, dxs, False), (H, dxd, False), (H, de, True)] if spec.gmp_order else \
-                [(H, de, True), (H, dxs, False), (H, dxd, False)]
-        nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
-                     acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e, ln_g=es.lnp()[0] if es.ln else None,
-                     hpre=ehp, stats=est, din=din, ln_partial=part_e, tag="edge_bwd",
-                     cost=with_alg(alg8d_edge(E, N, H, x.element_size(), bwd=True),
-                                   (cost_edge_bwd if spec.trick else cost_edge_bwd_cat)(E, N, H, x.element_size(), es.nlin)))
-        g0 = gpre_e[0]
+            gpre_e = _alloc_gpre(es, E, dt, dev, rowmajor=(0,) if spec.trick else ())
+            if spec.trick:
+                din = [(H, de, True)]
+            else:
+                dxs = torch.empty(E, H, dtype=dt, device=dev)
+                dxd = torch.empty(E, H, dtype=dt, device=dev)
+                din = [(H, dxs, False), (H, dxd, False), (H, de, True)] if spec.gmp_order else \
+                    [(H, de, True), (H, dxs, False), (H, dxd, False)]
+            nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim,
+                                wtpk=es.wtpk(), acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e,
+                                ln_g=es.lnp()[0] if es.ln else None, hpre=ehp, stats=est, din=din, ln_partial=part_e,
+                                tag="edge_bwd",
+                                cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True),
+                                              (cost_edge_bwd if spec.trick else cost_edge_bwd_cat)(E, N, H, sz,
+                                                                                                   es.nlin)))
+            g0 = gpre_e[0]
         grads_edge = []
         if spec.trick:
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
@@ -422,9 +439,18 @@ class GMPFn(torch.autograd.Function):
             mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
                         wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
-            eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e)
             eb = spec.eb
             wg = WGrad()
+            if fused:
+                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)  # filled by wg.run()
+                wg.add(g0, e, dwe)
+                eg = [dwe]
+                for l in range(3):
+                    eg += [dW13[l], db13[l]]
+                eg = eg[:1] + [t if t.dtype == p.dtype else t.to(p.dtype) for t, p in zip(eg[1:], es.params()[1:7])]
+                eg += list(_ln_grads(part_e, nb_e, H, es.ln[0].dtype))
+            else:
+                eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e, wg)
             dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dbd = torch.empty(H, dtype=torch.float32, device=dev)
@@ -432,6 +458,8 @@ class GMPFn(torch.autograd.Function):
             wg.add(dPd, x, dwd, dbd)
             grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n, wg)
             wg.run()
+            if fused:
+                eg[0] = eg[0] if eg[0].dtype == es.linears[0][0].dtype else eg[0].to(es.linears[0][0].dtype)
             grads_edge = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
             return (dx, de, None, None, None, *grads_edge, *grads_node)
         else:

@@ -363,6 +363,19 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   return launch_status();
 }
 
+int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream) {
+  if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD || nsplit < 1) return AGN_E_ARG;
+  int maxq = 1;
+  for (int i = 0; i < b->n; ++i) {
+    const int kpad = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    const int mpad = ((b->d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, b->n), dim3(64 * RED_G), 0, (hipStream_t)stream, *b,
+                     nsplit);
+  return launch_status();
+}
+
 int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, float* out, void* stream) {
   if (nw < 0 || n < 1 || scratch_rows < 1) return AGN_E_ARG;
   hipStream_t st = (hipStream_t)stream;

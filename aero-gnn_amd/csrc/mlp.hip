@@ -1071,7 +1071,9 @@ bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
   // edge/node chains with an H-wide dX, or any chain without dX (the edge encoder: d_e = 4 in)
   bool need_dx = false;
   for (int s = 0; s < a->din_nseg; ++s) need_dx |= a->din[s] != nullptr;
-  const bool din_ok = need_dx ? (a->din_nseg == 1 && a->in_dim == 128 && a->din_k[0] == 128) : a->nlin > 1;
+  // nlin == 1 with LayerNorm and no dX: the LayerNorm backward alone (G3 for agn_edge_bwd_fused)
+  const bool din_ok = need_dx ? (a->din_nseg == 1 && a->in_dim == 128 && a->din_k[0] == 128)
+                              : (a->nlin > 1 || a->use_ln);
   return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
          din_ok && a->rows >= 64 * 1024;
 }

@@ -309,6 +309,39 @@ int agn_wec_blocks(int n);
 int agn_wec_forward(const agn_wec_args* a, void* stream);
 int agn_wec_backward(const agn_wec_args* a, void* stream);
 
+/* ---- fused edge-MLP backward with in-kernel weight gradients (bf16, H = 128, the sum-trick
+ * EdgeBlockSum chain h0 = e W_e^T + P_s[src] + P_d[dst] -> ReLU -> Lin1 -> ReLU -> Lin2 -> ReLU
+ * -> Lin3 -> LayerNorm, mgnLayer.py:72-105, and the residual e' = e + ., mgnLayer.py:205).
+ * Replaces the chain part of agn_mlp_backward + agn_wgrad for that chain: given G3 = dL/dh3 (the
+ * LayerNorm backward, agn_mlp_backward with nlin = 1), one persistent launch runs the chain rule
+ * through Lin3..Lin1 and W_e and accumulates dW1..dW3 / db1..db3 in registers, so the
+ * pre-activation gradients G1, G2 are never written and G3 / the activations are read once.
+ * Outputs: de (with the residual gradient g + g2[gidx]), G0 = dL/dh0 (row-major; its sender /
+ * receiver segment sums are dP_s / dP_d, and dW_e = G0^T e goes to agn_wgrad), and per-block
+ * partials that agn_wgrad_reduce sums in fixed order. de and G0 are bitwise those of the split
+ * path; dW / db differ from it only in the fp32 order of the row sums. ---- */
+typedef struct {
+  int rows;                  /* edges (CSC order) */
+  int nblk;                  /* grid size: agn_edge_bwd_blocks() */
+  const void* wtpk[4];       /* packed A = W_l^T of W_e, Lin1, Lin2, Lin3 (agn_pack, bf16) */
+  const void* g;             /* [rows][128] grad of e' or NULL (unused output) */
+  const void* g2;            /* [N][128] dAgg (receiver-side grad) */
+  const int32_t* gidx;       /* [rows] receiver of each edge (row of g2) */
+  const void* g3;            /* AGN_TILED dL/dh3 (LayerNorm backward output) */
+  const void* act[3];        /* AGN_TILED a1, a2, a3 (ReLU outputs = inputs of Lin1..Lin3) */
+  const void* mask[3];       /* their AGN_RELU_MASK bits */
+  void* de;                  /* [rows][128] out: dL/de incl. the residual */
+  void* g0;                  /* [rows][128] out: dL/dh0 */
+  float* dw_partial;         /* [3][nblk][128][128]: dW1..dW3 slabs (agn_wgrad slab order) */
+  float* db_partial;         /* [3][nblk][128] */
+  unsigned long long* stamps; /* diagnostics only: NULL, or [2][4][8][32] s_memtime per phase */
+} agn_edge_bwd_args;
+int agn_edge_bwd_blocks(int rows);
+int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
+/* dw[m][k] = sum_s dw_partial[s][m][k] (and db) for each desc: the fixed-order second stage
+ * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
+int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

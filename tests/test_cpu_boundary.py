@@ -36,7 +36,8 @@ def test_struct_layouts_match_c(tmp_path):
                                                  "din_resid", "ln_partial"]),
               "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db"]),
               "agn_wgrad_batch": (L.WgradBatch, ["n", "d"]),
-              "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")])}
+              "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")]),
+              "agn_edge_bwd_args": (L.EdgeBwdArgs, [f for f, _ in L.EdgeBwdArgs._fields_])}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "aerognn.h"', 'int main(void){']
     for st, (_, fs) in fields.items():
         lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')

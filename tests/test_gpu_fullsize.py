@@ -229,3 +229,35 @@ def test_relu_mask_matches_saved_activations(rows, dtype):
         ok = r < rows
         expect = pos[np.minimum(r, rows - 1), np.broadcast_to(f, r.shape)]
         assert np.array_equal(bits.astype(bool)[ok], expect[ok])
+
+
+@pytest.mark.parametrize("E", [98_400, 70_001])  # ragged last round / ragged last tile
+def test_fused_edge_bwd_matches_split(E, monkeypatch):
+    """agn_edge_bwd_fused (LayerNorm backward pass + one persistent chain/dW kernel) against the
+    split path (agn_mlp_backward + agn_wgrad): activations, dx and de bitwise equal (same MFMA
+    order per row), parameter gradients equal up to the fp32 order of the row sums."""
+    from aerognn.graph import Level
+    from models.mgnLayer import MeshGraphNetLayer
+    m = _mesh(150, 110)
+    ei = m["edge_index"][:, :E].to(DEV)
+    N = m["x"].shape[0]
+    torch.manual_seed(0)
+    layer = MeshGraphNetLayer(128, 128, 128, 2, 2, do_concat_trick=True).to(DEV)
+    lv = Level.from_edge_index(ei, N)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(N, 128, generator=g).to(DEV, torch.bfloat16)
+    e = torch.randn(E, 128, generator=g).to(DEV, torch.bfloat16)
+    monkeypatch.setenv("AEROGNN_FUSED_EDGE_BWD", "1")
+    fused = _layer_step(layer, x, e, lv)
+    monkeypatch.setenv("AEROGNN_FUSED_EDGE_BWD", "0")
+    split = _layer_step(layer, x, e, lv)
+    for name, a, b in zip(("x'", "e'", "dx", "de"), fused[:4], split[:4]):
+        r = rel_l2(a.float(), b.double())
+        print(f"{name}: rel-L2 {r:.2e}, differing {float((a != b).float().mean()):.2e}")
+        assert torch.equal(a, b), (name, r)
+    worst = 0.0
+    for n in fused[4]:
+        r = rel_l2(fused[4][n].float(), split[4][n].double())
+        worst = max(worst, r)
+        print(f"{n:45s} rel-L2 {r:.2e}")
+    assert worst <= 1e-5, worst
