@@ -59,7 +59,7 @@ MAX_WGRAD = 8
 class WgradDesc(C.Structure):
     _fields_ = [("g", vp), ("x", vp), ("ldg", i32), ("ldx", i32), ("m", i32), ("k", i32), ("rows", i32),
                 ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp),
-                ("g_tiled", i32), ("x_tiled", i32)]
+                ("g_tiled", i32), ("x_tiled", i32), ("nsplit", i32), ("_pad", i32)]
 
 
 class WgradBatch(C.Structure):
@@ -99,7 +99,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_collate",
-            "agn_global_pool", "agn_edge_bwd_fused", "agn_wgrad_reduce")
+            "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce")
 
 
 class AeroGNNError(RuntimeError):
@@ -159,9 +159,12 @@ def lib():
             "agn_wgrad_nsplit": (i32, [i32, i32]),
             "agn_wgrad_partial_floats": (C.c_size_t, [i32, i32, i32]),
             "agn_wgrad": (i32, [C.POINTER(WgradBatch), i32, i32, vp]),
+            "agn_wgrad_plan": (i32, [C.POINTER(WgradBatch)]),
             "agn_colsum": (i32, [vp, i32, i32, vp, i32, vp, vp]),
             "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
             "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
+            "agn_segment_max": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, vp]),
+            "agn_segment_max_backward": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
             "agn_radix_sort_temp_bytes": (C.c_size_t, [i32]),
             "agn_radix_sort_u64": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
             "agn_row_ptr": (i32, [vp, i32, i32, vp, vp]),

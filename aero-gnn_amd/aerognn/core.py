@@ -294,7 +294,7 @@ def edge_bwd_fused(*, rows, wtpk, g, g2, gidx, g3, acts, de, g0, tag=None, cost=
     b.n = 3
     for l in range(3):
         b.d[l] = L.WgradDesc(None, None, H, H, H, H, int(rows), H, ptr(dwp[l * nblk * H * H:]), ptr(dbp[l * nblk * H:]),
-                             ptr(dw[l]), ptr(db[l]), 0, 0)
+                             ptr(dw[l]), ptr(db[l]), 0, 0, nblk, 0)
     check(lib.agn_wgrad_reduce(C.byref(b), nblk, stream()), "wgrad_reduce")
     return dw, db
 
@@ -308,6 +308,18 @@ def segment_sum(rows, k, ptr_t, perm, src, out, mean=False, src_ld=None, out_ld=
                                   src_ld or src.stride(0), ptr(out), out_ld or out.stride(0), int(mean),
                                   stream()), "segment_sum")
     return out
+
+
+def segment_max(rows, k, ptr_t, perm, src, out, argmax):
+    check(L.lib().agn_segment_max(rows, k, dt_code(src.dtype), ptr(ptr_t), ptr(perm), ptr(src), src.stride(0), ptr(out),
+                                  out.stride(0), ptr(argmax), stream()), "segment_max")
+    return out
+
+
+def segment_max_backward(rows, k, argmax, gout, dx):
+    check(L.lib().agn_segment_max_backward(rows, k, dt_code(gout.dtype), ptr(argmax), ptr(gout), gout.stride(0), ptr(dx),
+                                           dx.stride(0), stream()), "segment_max_backward")
+    return dx
 
 
 def gather_rows(rows, k, idx, src, out, cnt_ptr=None, add=None):
@@ -351,33 +363,36 @@ class WGrad:
         lib = L.lib()
         for i in range(0, len(self.items), L.MAX_WGRAD):
             chunk = self.items[i:i + L.MAX_WGRAD]
-            rows = max(logical_rows(it[0]) for it in chunk)
             dev = chunk[0][0].device
-            if rows == 0:
-                for G, X, dw, db in chunk:
+            live = []
+            for G, X, dw, db in chunk:
+                if logical_rows(G) == 0:
                     dw.zero_()
                     if db is not None:
                         db.zero_()
+                else:
+                    live.append((G, X, dw, db))
+            if not live:
                 continue
-            nblk = sum(((it[0].shape[1] + 127) // 128) * ((it[1].shape[1] + 127) // 128) for it in chunk)
-            ns = int(lib.agn_wgrad_nsplit(rows, nblk))
-            sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], ns)) for G, X, _, _ in chunk]
-            bsz = [ns * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0 for G, _, _, db in chunk]
-            scratch = torch.empty(sum(sizes) + sum(bsz), dtype=torch.float32, device=dev)
             b = L.WgradBatch()
-            b.n = len(chunk)
-            o = 0
-            for j, (G, X, dw, db) in enumerate(chunk):
-                dwp = scratch[o:o + sizes[j]]
-                o += sizes[j]
-                dbp = None
-                if db is not None:
-                    dbp = scratch[o:o + bsz[j]]
-                    o += bsz[j]
+            b.n = len(live)
+            for j, (G, X, dw, db) in enumerate(live):
                 b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], logical_rows(G),
-                                     dw.stride(0), ptr(dwp), ptr(dbp), ptr(dw), ptr(db), int(is_tiled(G)),
-                                     int(is_tiled(X)))
-            check(lib.agn_wgrad(C.byref(b), dt_code(chunk[0][0].dtype), ns, stream()), "wgrad")
+                                     dw.stride(0), None, None, ptr(dw), ptr(db), int(is_tiled(G)), int(is_tiled(X)), 0, 0)
+            check(lib.agn_wgrad_plan(C.byref(b)), "wgrad_plan")  # splits in proportion to rows
+            sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], b.d[j].nsplit))
+                     for j, (G, X, _, _) in enumerate(live)]
+            bsz = [b.d[j].nsplit * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0
+                   for j, (G, _, _, db) in enumerate(live)]
+            scratch = torch.empty(sum(sizes) + sum(bsz), dtype=torch.float32, device=dev)
+            o = 0
+            for j, (G, X, dw, db) in enumerate(live):
+                b.d[j].dw_partial = ptr(scratch[o:o + sizes[j]])
+                o += sizes[j]
+                if db is not None:
+                    b.d[j].db_partial = ptr(scratch[o:o + bsz[j]])
+                    o += bsz[j]
+            check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
         self.items = []
 
 

@@ -24,7 +24,7 @@ from ._lib import check, ptr
 from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_bwd_ok, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
-                   scatter_rows, segment_sum, stream)
+                   scatter_rows, segment_max, segment_max_backward, segment_sum, stream)
 
 
 def _c(t):
@@ -915,3 +915,89 @@ class WECGivenFn(torch.autograd.Function):
         wg.run()
         T = spec.mod.transform
         return (dx, dw, None, None, None, dT.to(T.weight.dtype), dTb.to(T.bias.dtype))
+
+
+# --------------------------------------------------------------------------- global pooling
+class GraphGroups:
+    """Node grouping by graph id for global pooling (poolmgn.py:132-141): `perm`/`rowptr` group the
+    nodes of each graph 0..G-1 (stable, any batch order; G = batch.max() + 1 as PyG's global pools
+    size it), `bcast` is the row index of the reference's broadcast back to nodes,
+    `pooled.repeat_interleave(bincount(batch))` (= batch itself when batch is sorted), `bptr` the
+    CSR grouping of `bcast` (contiguous by construction) for the broadcast backward."""
+
+    def __init__(self, batch, n, device):
+        from .graph import group_by
+        if batch is None:
+            self.G = 1
+            self.perm = None
+            self.rowptr = torch.tensor([0, n], dtype=torch.int32, device=device)
+            self.bcast = torch.zeros(n, dtype=torch.int32, device=device)
+            self.bptr = self.rowptr
+            return
+        b32 = batch.to(torch.int32)
+        self.G = int(batch.max().item()) + 1 if n > 0 else 0
+        self.perm, self.rowptr = group_by(b32, self.G)
+        counts = self.rowptr[1:] - self.rowptr[:-1]
+        self.bcast = torch.repeat_interleave(torch.arange(self.G, dtype=torch.int32, device=device), counts)
+        self.bptr = self.rowptr  # bcast rows of graph g are rowptr[g]..rowptr[g+1]-1
+
+
+class GlobalPoolFn(torch.autograd.Function):
+    """global_{mean,add,max}_pool(x, batch) (torch_geometric; poolmgn.py:38-45) on libaerognn:
+    segment sum / mean (fixed member order) or segment max with first-argmax backward."""
+
+    @staticmethod
+    def forward(ctx, x, groups, method):
+        x = _c(x)
+        G, k = groups.G, x.shape[1]
+        out = torch.empty(G, k, dtype=x.dtype, device=x.device)
+        ctx.groups, ctx.method, ctx.n = groups, method, x.shape[0]
+        if method in ("mean", "add"):
+            segment_sum(G, k, groups.rowptr, groups.perm, x, out, mean=(method == "mean"))
+        elif method == "max":
+            arg = torch.empty(G, k, dtype=torch.int32, device=x.device)
+            segment_max(G, k, groups.rowptr, groups.perm, x, out, arg)
+            ctx.arg = arg
+        else:
+            raise ValueError(f"Unsupported global pooling method: {method}")
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        grp = ctx.groups
+        g = _c(g)
+        k = g.shape[1]
+        if ctx.method == "max":
+            dx = torch.zeros(ctx.n, k, dtype=g.dtype, device=g.device)
+            segment_max_backward(grp.G, k, ctx.arg, g, dx)
+            return dx, None, None
+        # d x[i] = g[graph(i)] (/ count for mean): a row gather through the node -> graph map
+        node_graph = torch.empty(ctx.n, dtype=torch.int32, device=g.device)
+        if grp.perm is None:
+            node_graph.zero_()
+        else:
+            node_graph[grp.perm.long()] = grp.bcast
+        dx = torch.empty(ctx.n, k, dtype=g.dtype, device=g.device)
+        gather_rows(ctx.n, k, node_graph, g, dx, cnt_ptr=grp.rowptr if ctx.method == "mean" else None)
+        return dx, None, None
+
+
+class BroadcastRowsFn(torch.autograd.Function):
+    """pooled.repeat_interleave(bincount(batch), dim=0) (poolmgn.py:134): y[i] = pooled[bcast[i]];
+    backward = per-graph segment sum of the row gradients (contiguous groups)."""
+
+    @staticmethod
+    def forward(ctx, pooled, groups):
+        pooled = _c(pooled)
+        n = groups.bcast.numel()
+        out = torch.empty(n, pooled.shape[1], dtype=pooled.dtype, device=pooled.device)
+        gather_rows(n, pooled.shape[1], groups.bcast, pooled, out)
+        ctx.groups, ctx.G = groups, pooled.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        dp = torch.empty(ctx.G, g.shape[1], dtype=g.dtype, device=g.device)
+        segment_sum(ctx.G, g.shape[1], ctx.groups.bptr, None, g, dp)
+        return dp, None

@@ -131,19 +131,28 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
   return r;
 }
 
-// grid: x = row chunk (split), y = M block * nKb + K block, z = desc
+// grid.x = sum over descs of nsplit_d * (output blocks of d): blockIdx.x -> (desc, split, block),
+// descs in order, each desc's blocks split-major. Splits per desc are in proportion to its rows
+// (agn_wgrad_plan), so a small (node-row) desc does not idle while a large (edge-row) one runs.
 template <typename T>
-__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
+__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
   __shared__ __attribute__((aligned(16))) T sx[DW_ROWS * LD];
-  const agn_wgrad_desc& d = b.d[blockIdx.z];
+  int di = 0, local = blockIdx.x;
+  for (; di < b.n; ++di) {
+    const int nb = ((b.d[di].m + DW_BLK - 1) / DW_BLK) * ((b.d[di].k + DW_BLK - 1) / DW_BLK) * b.d[di].nsplit;
+    if (local < nb) break;
+    local -= nb;
+  }
+  if (di >= b.n) return;
+  const agn_wgrad_desc& d = b.d[di];
+  const int nsplit = d.nsplit;
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK;
   const int nMb = (d.m + DW_BLK - 1) / DW_BLK;
-  if ((int)blockIdx.y >= nMb * nKb) return;
-  const int mb = blockIdx.y / nKb, kb = blockIdx.y % nKb;
+  const int split = local / (nMb * nKb), blk = local - split * (nMb * nKb);
+  const int mb = blk / nKb, kb = blk % nKb;
   const int m0 = mb * DW_BLK, k0 = kb * DW_BLK;
-  const int split = blockIdx.x;
   const int per = ((d.rows + nsplit - 1) / nsplit + DW_ROWS - 1) / DW_ROWS * DW_ROWS;
   const int rbeg = split * per, rend = min(d.rows, rbeg + per);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -228,10 +237,11 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
 // g + RED_G, ... and the group partials are combined in LDS in group order: a fixed
 // summation order (deterministic), with RED_G x 64 16-B loads in flight per block.
 constexpr int RED_G = 8;
-__global__ __launch_bounds__(64 * RED_G) void wgrad_reduce_kernel(const agn_wgrad_batch b, int nsplit) {
+__global__ __launch_bounds__(64 * RED_G) void wgrad_reduce_kernel(const agn_wgrad_batch b) {
   __shared__ f32x4 part[RED_G][64];
   __shared__ float bpart[RED_G][64];
   const agn_wgrad_desc& d = b.d[blockIdx.y];
+  const int nsplit = d.nsplit;
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK, nMb = (d.m + DW_BLK - 1) / DW_BLK;
   const int kpad = nKb * DW_BLK, mpad = nMb * DW_BLK;
   const size_t slab = (size_t)mpad * kpad;
@@ -315,9 +325,8 @@ inline int launch_status() {
 
 extern "C" {
 
-int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
-  // exactly one full wave of resident workgroups over all descriptors/blocks (no tail wave),
-  // >= 2 LDS stages per split
+namespace {
+int wgrad_resident() {
   static int resident = 0;
   if (resident == 0) {
     int dev = 0, ncu = 256, per = 3;
@@ -327,7 +336,15 @@ int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
       per = 3;
     resident = ncu * per;
   }
-  int ns = resident / (ndesc_blocks > 0 ? ndesc_blocks : 1);
+  return resident;
+}
+int out_blocks(const agn_wgrad_desc& d) { return ((d.m + DW_BLK - 1) / DW_BLK) * ((d.k + DW_BLK - 1) / DW_BLK); }
+}  // namespace
+
+int agn_wgrad_nsplit(int rows, int ndesc_blocks) {
+  // exactly one full wave of resident workgroups over all descriptors/blocks (no tail wave),
+  // >= 2 LDS stages per split
+  int ns = wgrad_resident() / (ndesc_blocks > 0 ? ndesc_blocks : 1);
   const int maxs = (rows + 2 * DW_ROWS - 1) / (2 * DW_ROWS);
   if (ns > maxs) ns = maxs;
   return ns < 1 ? 1 : ns;
@@ -338,41 +355,54 @@ size_t agn_wgrad_partial_floats(int m, int k, int nsplit) {
   return (size_t)nsplit * mp * kp;
 }
 
-int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
-  if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD || nsplit < 1) return AGN_E_ARG;
-  int maxblk = 1;
+int agn_wgrad_plan(agn_wgrad_batch* b) {
+  // One wave of resident workgroups. Splits are uniform across the descs of a batch: the kernel is
+  // HBM-bound, so a desc whose splits finish early leaves bandwidth to the others; splitting in
+  // proportion to rows measured 6 % slower at C3 (more, shorter splits) and is not used.
+  if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD) return AGN_E_ARG;
+  int nblk = 0, rows = 0;
   for (int i = 0; i < b->n; ++i) {
-    const agn_wgrad_desc& d = b->d[i];
+    nblk += out_blocks(b->d[i]);
+    rows = b->d[i].rows > rows ? b->d[i].rows : rows;
+  }
+  const int ns = agn_wgrad_nsplit(rows, nblk);
+  for (int i = 0; i < b->n; ++i) b->d[i].nsplit = ns;
+  return 0;
+}
+
+int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
+  if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD) return AGN_E_ARG;
+  agn_wgrad_batch bb = *b;
+  int total = 0, maxq = 1;
+  for (int i = 0; i < bb.n; ++i) {
+    agn_wgrad_desc& d = bb.d[i];
     if (d.m < 1 || d.k < 1 || d.rows < 0) return AGN_E_ARG;
     if ((d.g_tiled && d.m != DW_BLK) || (d.x_tiled && d.k != DW_BLK)) return AGN_E_SHAPE;
-    const int nb = ((d.m + DW_BLK - 1) / DW_BLK) * ((d.k + DW_BLK - 1) / DW_BLK);
-    maxblk = nb > maxblk ? nb : maxblk;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  dim3 grid(nsplit, maxblk, b->n);
-  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
-  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, *b, nsplit);
-  else return AGN_E_DTYPE;
-  int maxq = 1;  // column quads of the largest padded slab
-  for (int i = 0; i < b->n; ++i) {
-    const int kpad = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK;
-    const int mpad = ((b->d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    if (nsplit > 0) d.nsplit = nsplit;
+    if (d.nsplit < 1) return AGN_E_ARG;
+    total += out_blocks(d) * d.nsplit;
+    const int kpad = ((d.k + DW_BLK - 1) / DW_BLK) * DW_BLK, mpad = ((d.m + DW_BLK - 1) / DW_BLK) * DW_BLK;
     maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, b->n), dim3(64 * RED_G), 0, st, *b, nsplit);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, dim3(total), dim3(DW_THREADS), 0, st, bb);
+  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, dim3(total), dim3(DW_THREADS), 0, st, bb);
+  else return AGN_E_DTYPE;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
   return launch_status();
 }
 
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream) {
   if (!b || b->n < 1 || b->n > AGN_MAX_WGRAD || nsplit < 1) return AGN_E_ARG;
+  agn_wgrad_batch bb = *b;
   int maxq = 1;
-  for (int i = 0; i < b->n; ++i) {
-    const int kpad = ((b->d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK;
-    const int mpad = ((b->d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
+  for (int i = 0; i < bb.n; ++i) {
+    bb.d[i].nsplit = nsplit;
+    const int kpad = ((bb.d[i].k + DW_BLK - 1) / DW_BLK) * DW_BLK;
+    const int mpad = ((bb.d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
     maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, b->n), dim3(64 * RED_G), 0, (hipStream_t)stream, *b,
-                     nsplit);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, (hipStream_t)stream, bb);
   return launch_status();
 }
 

@@ -95,6 +95,44 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   }
 }
 
+// Global max pooling (torch_geometric global_max_pool = scatter 'max' over graph ids, poolmgn.py:40):
+// out[r][f] = max over the members j of group r of src[perm[j]][f] (0 for an empty group, as the
+// zero-initialised scatter_reduce(include_self=False) leaves it), argmax[r][f] = the FIRST member
+// row attaining it (-1 if empty) for the backward. One thread per (group, feature); members are
+// walked in index order. NaN propagates (any NaN member makes the max NaN, first NaN wins).
+template <typename T>
+__global__ __launch_bounds__(256) void segment_max_kernel(int rows, int k, const int32_t* __restrict__ ptr,
+                                                          const int32_t* __restrict__ perm, const T* __restrict__ src,
+                                                          int src_ld, T* __restrict__ out, int out_ld,
+                                                          int32_t* __restrict__ argmax) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)rows * k) return;
+  const int r = (int)(t / k), f = (int)(t - (long)r * k);
+  const int beg = ptr[r], end = ptr[r + 1];
+  float best = 0.f;
+  int arg = -1;
+  for (int j = beg; j < end; ++j) {
+    const int e = perm ? perm[j] : j;
+    const float v = to_f(src[(size_t)e * src_ld + f]);
+    if (arg < 0 || v > best || (v != v && best == best)) { best = v; arg = e; }
+  }
+  out[(size_t)r * out_ld + f] = from_f<T>(best);
+  argmax[(size_t)r * k + f] = arg;
+}
+
+// backward of segment_max: dx[argmax[r][f]][f] = gout[r][f] (dx zero-filled by the caller; the
+// argmax rows of different groups are disjoint, so no two threads write one element)
+template <typename T>
+__global__ __launch_bounds__(256) void segment_max_bwd_kernel(int rows, int k, const int32_t* __restrict__ argmax,
+                                                              const T* __restrict__ gout, int gout_ld,
+                                                              T* __restrict__ dx, int dx_ld) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)rows * k) return;
+  const int r = (int)(t / k), f = (int)(t - (long)r * k);
+  const int a = argmax[t];
+  if (a >= 0) dx[(size_t)a * dx_ld + f] = gout[(size_t)r * gout_ld + f];
+}
+
 // out[r] = src[idx[r]] / (cnt_ptr ? max(cnt_ptr[idx+1]-cnt_ptr[idx],1) : 1) + (add ? add[r] : 0)
 template <typename T>
 __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const int32_t* __restrict__ idx,
@@ -504,6 +542,44 @@ int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_
   if (dtype == AGN_F32) return seg_sum_t<float>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   return AGN_E_DTYPE;
+}
+
+int agn_segment_max(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm, const void* src, int src_ld,
+                    void* out, int out_ld, int32_t* argmax, void* stream) {
+  if (rows < 0 || k < 1 || !argmax) return AGN_E_ARG;
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)rows * k;
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (dtype == AGN_F32)
+    hipLaunchKernelGGL(segment_max_kernel<float>, g, dim3(256), 0, st, rows, k, ptr, perm, (const float*)src, src_ld,
+                       (float*)out, out_ld, argmax);
+  else if (dtype == AGN_BF16)
+    hipLaunchKernelGGL(segment_max_kernel<bf16>, g, dim3(256), 0, st, rows, k, ptr, perm, (const bf16*)src, src_ld,
+                       (bf16*)out, out_ld, argmax);
+  else
+    return AGN_E_DTYPE;
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int agn_segment_max_backward(int rows, int k, int dtype, const int32_t* argmax, const void* gout, int gout_ld,
+                             void* dx, int dx_ld, void* stream) {
+  if (rows < 0 || k < 1 || !argmax) return AGN_E_ARG;
+  if (rows == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const long n = (long)rows * k;
+  const dim3 g((unsigned)((n + 255) / 256));
+  if (dtype == AGN_F32)
+    hipLaunchKernelGGL(segment_max_bwd_kernel<float>, g, dim3(256), 0, st, rows, k, argmax, (const float*)gout, gout_ld,
+                       (float*)dx, dx_ld);
+  else if (dtype == AGN_BF16)
+    hipLaunchKernelGGL(segment_max_bwd_kernel<bf16>, g, dim3(256), 0, st, rows, k, argmax, (const bf16*)gout, gout_ld,
+                       (bf16*)dx, dx_ld);
+  else
+    return AGN_E_DTYPE;
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
 }
 
 int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* src, int src_ld,

@@ -162,6 +162,8 @@ typedef struct {
   float* dw;            /* [m][ldw] fp32 output */
   float* db;            /* [m] fp32 output or NULL */
   int g_tiled, x_tiled; /* operand in the AGN_TILED layout (then m resp. k == 128) */
+  int nsplit;           /* row splits of this desc (agn_wgrad_plan); dw_partial holds nsplit slabs */
+  int _pad;
 } agn_wgrad_desc;
 typedef struct {
   int n;
@@ -170,6 +172,10 @@ typedef struct {
 } agn_wgrad_batch;
 int agn_wgrad_nsplit(int rows, int ndesc_blocks);
 size_t agn_wgrad_partial_floats(int m, int k, int nsplit);
+/* Fill d[i].nsplit: one wave of resident workgroups over the batch, the same split count for every
+ * desc (agn_wgrad_nsplit of the largest). Host-only, no launch. */
+int agn_wgrad_plan(agn_wgrad_batch* b);
+/* nsplit > 0: every desc uses nsplit splits; nsplit <= 0: each desc uses its own d[i].nsplit */
 int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream);
 /* out[c] = sum_r p[r][c] (r < nw, c < n) in fixed order via scratch[scratch_rows][n] */
 int agn_colsum(const float* p, int nw, int n, float* scratch, int scratch_rows, float* out, void* stream);
@@ -196,6 +202,14 @@ int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* s
 /* out[r] = sum (or mean) of src[perm ? perm[j] : j] for j in ptr[r]..ptr[r+1]-1; [rows][k] */
 int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm,
                     const void* src, int src_ld, void* out, int out_ld, int mean, void* stream);
+/* Global max pooling (poolmgn.py:40, torch_geometric global_max_pool = scatter 'max'):
+ * out[r][f] = max of src[perm ? perm[j] : j][f], j in ptr[r]..ptr[r+1]-1 (0 if empty), argmax[r][f]
+ * = the first member row attaining it (-1 if empty); the backward writes dx[argmax[r][f]][f] =
+ * gout[r][f] into a zero-filled dx. */
+int agn_segment_max(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm, const void* src,
+                    int src_ld, void* out, int out_ld, int32_t* argmax, void* stream);
+int agn_segment_max_backward(int rows, int k, int dtype, const int32_t* argmax, const void* gout, int gout_ld,
+                             void* dx, int dx_ld, void* stream);
 /* out[r] = src[idx[r]] * (inv_count ? 1/max(cnt[idx[r]],1) : 1) + (add ? add[r] : 0) */
 int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* src, int src_ld,
                     const int32_t* cnt_ptr, const void* add, int add_ld, void* out, int out_ld,

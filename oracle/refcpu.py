@@ -201,6 +201,37 @@ def bsms_forward(p, x, ea, ei, cfg, batch=None, pos=None, stable=False):
     return mlp(p, "decoder", cn, mlp_nlin(cfg["n_hid_dec"]), ln=False)
 
 
+# torch_geometric.nn.global_{add,mean,max}_pool (PyG; unpinned, not installed): size = batch.max()+1,
+# scatter 'sum' / 'mean' (count clamped to 1) / 'max' (zero-initialised amax, include_self=False)
+def global_pool(x, batch, method):
+    size = int(batch.max()) + 1
+    idx = batch.view(-1, 1).expand_as(x)
+    out = x.new_zeros(size, x.size(1))
+    if method == "max":
+        return out.scatter_reduce_(0, idx, x, reduce="amax", include_self=False)
+    out = out.scatter_add_(0, idx, x)
+    if method == "mean":
+        cnt = x.new_zeros(size).scatter_add_(0, batch, x.new_ones(x.size(0))).clamp_(min=1)
+        out = out / cnt.view(-1, 1)
+    return out
+
+
+# models/poolmgn.py:120-158 (poolMGN.forward)
+def poolmgn_forward(p, x, ea, ei, cfg, batch=None):
+    g = mlp(p, "global_encoder", x, mlp_nlin(cfg["n_hid_global_enc"]), ln=False)
+    if batch is not None:
+        g = global_pool(g, batch, cfg["global_pool_method"])
+        g = g.repeat_interleave(torch.bincount(batch), dim=0)
+    else:
+        g = global_pool(g, torch.zeros(x.size(0), dtype=torch.long), cfg["global_pool_method"])
+        g = g.repeat(x.size(0), 1)
+    xh = mlp(p, "node_encoder", torch.cat((x, g), dim=-1), mlp_nlin(cfg["n_hid_node_enc"]))
+    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]))
+    for l in range(cfg["processor_size"]):
+        xh, eh = gmp_layer(p, f"layers.{l}", xh, eh, ei, cfg)
+    return mlp(p, "decoder", xh, mlp_nlin(cfg["n_hid_dec"]), ln=False)
+
+
 def cfg_from_kwargs(**kw):
     """Map BiStridedMeshGraphNet / MeshGraphNet ctor kwargs (reference names) to oracle cfg."""
     return dict(
@@ -215,4 +246,6 @@ def cfg_from_kwargs(**kw):
         num_scales=kw.get("num_scales", 3),
         layers_per_scale=kw.get("layers_per_scale", 2),
         stride=kw.get("stride", 2),
+        global_pool_method=kw.get("global_pool_method", "mean"),
+        n_hid_global_enc=kw.get("num_hidden_layers_global_encoder", 1),
     )

@@ -122,3 +122,17 @@ def test_cpu_tensors_fail_loudly():
     ei = torch.randint(0, 10, (2, 20))
     with pytest.raises(RuntimeError):
         layer(x, e, ei)
+
+
+def test_poolmgn_state_dict_and_errors():
+    """poolMGN keeps the reference's module tree (state_dict keys of the golden, generated from
+    /root/reference/models/poolmgn.py) and its ValueError for an unknown pooling method."""
+    from golden_util import load as _load
+    from models.poolmgn import poolMGN
+    d, m = _load("poolmgn_mean")
+    model = poolMGN(*m["dims"], **m["kwargs"])
+    ref_keys = sorted(k[2:] for k in d if k.startswith("p:"))
+    assert sorted(model.state_dict().keys()) == ref_keys
+    model.load_state_dict(params(d))
+    with pytest.raises(ValueError):
+        poolMGN(6, 4, 4, global_pool_method="median")

@@ -281,3 +281,40 @@ def test_native_lib_loaded():
     import aerognn._lib as L
     _lib_loaded()
     assert L._lib is not None
+
+
+# ------------------------------------------------------------------------------ poolMGN (§8f row 4)
+@pytest.mark.parametrize("method", ["mean", "max", "add"])
+def test_poolmgn(method):
+    """models/poolmgn.py: global encoder -> global_{mean,max,add}_pool -> broadcast -> concat ->
+    MeshGraphNet, vs the reference's goldens (forward and parameter grads)."""
+    from models.poolmgn import poolMGN
+    d, m = load(f"poolmgn_{method}")
+    model = _load(_model_from(m, poolMGN), d)
+    pred = model(d["x"].to(DEV), d["edge_attr"].to(DEV), d["edge_index"].to(DEV), batch=d["batch"].to(DEV))
+    _fwd_ok(pred, d["pred"])
+    torch.nn.functional.mse_loss(pred, d["y"].to(DEV)).backward()
+    _check_param_grads(model, d)
+
+
+@pytest.mark.parametrize("method", ["mean", "max"])
+def test_poolmgn_h128_vs_oracle(method):
+    """H = 128 poolMGN on a 3-mesh batch (unequal sizes) and without `batch`, vs the oracle."""
+    from aerognn.meshgen import collate, ellipsoid
+    from models.poolmgn import poolMGN
+    from oracle import refcpu as R
+    b = collate([ellipsoid(30, 20, seed=s) for s in (0, 1)] + [ellipsoid(24, 12, seed=2)])
+    t = {k: torch.from_numpy(v) for k, v in b.items()}
+    kw = dict(processor_size=4, num_hidden_layers_node_processor=2, num_hidden_layers_edge_processor=2,
+              num_hidden_layers_node_encoder=2, num_hidden_layers_edge_encoder=2, num_hidden_layers_decoder=2,
+              aggregation="add", global_pool_method=method, num_hidden_layers_global_encoder=1, global_dim=128)
+    torch.manual_seed(0)
+    model = poolMGN(6, 4, 4, **kw).to(DEV)
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    cfg = R.cfg_from_kwargs(**kw)
+    for batch in (t["batch"], None):
+        pred = model(t["x"].to(DEV), t["edge_attr"].to(DEV), t["edge_index"].to(DEV),
+                     batch=batch.to(DEV) if batch is not None else None)
+        with torch.no_grad():
+            ref = R.poolmgn_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch)
+        _fwd_ok(pred, ref)

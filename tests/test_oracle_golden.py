@@ -131,3 +131,15 @@ def test_downsample_nopos():
                                             None, m["stride"])
     assert torch.equal(f2c, d["f2c"]) and torch.equal(cei, d["c_edge_index"])
     assert torch.equal(cn, d["c_node"]) and torch.equal(ce, d["c_edge"])
+
+
+@pytest.mark.parametrize("method", ["mean", "max", "add"])
+def test_poolmgn(method):
+    """poolMGN (models/poolmgn.py) with the restated torch_geometric global pools."""
+    d, m = load(f"poolmgn_{method}")
+    p = _leaf(params(d))
+    cfg = R.cfg_from_kwargs(**m["kwargs"])
+    pred = R.poolmgn_forward(p, d["x"], d["edge_attr"], d["edge_index"], cfg, d["batch"])
+    assert torch.equal(pred, d["pred"]) or rel_l2(pred, d["pred"]) <= FWD_TOL
+    torch.nn.functional.mse_loss(pred, d["y"]).backward()
+    _check_grads(p, d)

@@ -52,8 +52,28 @@ def _install_standins():
     ts.scatter_sum = scatter_add
     tg = types.ModuleType("torch_geometric")
     tgn = types.ModuleType("torch_geometric.nn")
-    for n in ("global_mean_pool", "global_max_pool", "global_add_pool"):
-        setattr(tgn, n, lambda *a, **k: (_ for _ in ()).throw(RuntimeError("stand-in")))
+
+    # torch_geometric.nn.global_{add,mean,max}_pool (unpinned version, not installed here), restated
+    # from PyG's published algorithm: size = batch.max() + 1; torch_geometric.utils.scatter with
+    # reduce 'sum' (scatter_add_), 'mean' (sum / count.clamp(min=1)), 'max' (zero-initialised
+    # scatter_reduce_('amax', include_self=False)). Used only by models/poolmgn.py.
+    def _pool(x, batch, reduce, size=None):
+        if batch is None:
+            batch = torch.zeros(x.size(0), dtype=torch.long, device=x.device)
+        size = int(batch.max()) + 1 if size is None else size
+        idx = batch.view(-1, 1).expand_as(x)
+        out = x.new_zeros(size, x.size(1))
+        if reduce == "max":
+            return out.scatter_reduce_(0, idx, x, reduce="amax", include_self=False)
+        out = out.scatter_add_(0, idx, x)
+        if reduce == "mean":
+            cnt = x.new_zeros(size).scatter_add_(0, batch, x.new_ones(x.size(0))).clamp_(min=1)
+            out = out / cnt.view(-1, 1)
+        return out
+
+    tgn.global_add_pool = lambda x, batch, size=None: _pool(x, batch, "sum", size)
+    tgn.global_mean_pool = lambda x, batch, size=None: _pool(x, batch, "mean", size)
+    tgn.global_max_pool = lambda x, batch, size=None: _pool(x, batch, "max", size)
     tg.nn = tgn
     sys.modules["torch_scatter"] = ts
     sys.modules["torch_geometric"] = tg
@@ -61,11 +81,19 @@ def _install_standins():
 
 
 _install_standins()
+# the reference's models/ (a namespace package: no __init__.py) must not be shadowed by this
+# repo's regular package aero-gnn_amd/models, which would win the import scan
+sys.path[:] = [p for p in sys.path if os.path.abspath(p) != os.path.abspath(os.path.join(os.path.dirname(__file__), "..",
+                                                                                            "aero-gnn_amd"))]
+sys.modules.pop("models", None)
 sys.path.insert(0, REF)
 from models.mlp import MLP  # noqa: E402
 from models.mgnLayer import EdgeBlock, EdgeBlockSum, NodeBlock, MeshGraphNetLayer  # noqa: E402
 from models.mgn import MeshGraphNet  # noqa: E402
 from models.bsms_mgn import BiStridedMeshGraphNet  # noqa: E402
+from models.poolmgn import poolMGN  # noqa: E402
+import models.mlp as _refcheck  # noqa: E402
+assert os.path.abspath(_refcheck.__file__).startswith(REF), _refcheck.__file__  # the REFERENCE's modules
 
 
 def _np(t):
@@ -267,8 +295,30 @@ def case_bf16():
          x_out=xo, e_out=eo, x_out_bf16=xb.float(), e_out_bf16=eb.float(), **sd(layer))
 
 
+def case_poolmgn():
+    """poolMGN (models/poolmgn.py) for each global pooling method on a 2-graph batch, H = 32."""
+    for method in ("mean", "max", "add"):
+        torch.manual_seed(8)
+        t = batch_tensors([(12, 8, 0), (10, 6, 1)])
+        kw = dict(MODEL_KW, processor_size=3, aggregation="add", global_pool_method=method,
+                  num_hidden_layers_global_encoder=1, global_dim=32)
+        kw.pop("do_concat_trick", None)
+        for k in ("num_scales", "layers_per_scale", "stride"):
+            kw.pop(k, None)
+        m = poolMGN(6, 4, 4, **kw)
+        pred = m(t["x"], t["edge_attr"], t["edge_index"], batch=t["batch"])
+        loss = torch.nn.MSELoss()(pred, t["y"])
+        loss.backward()
+        save(f"poolmgn_{method}", dict(kwargs=kw, dims=[6, 4, 4]), x=t["x"], edge_attr=t["edge_attr"],
+             edge_index=t["edge_index"], batch=t["batch"], y=t["y"], pred=pred, loss=loss, **sd(m), **grads(m))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:  # selected cases only, e.g. `python tools/make_goldens.py poolmgn`
+        for c in sys.argv[1:]:
+            globals()[f"case_{c}"]()
+        sys.exit(0)
     case_mlp()
     case_blocks()
     case_layer("layer_sum_h32", 32, 10, 6, True)
