@@ -98,7 +98,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_exclusive_scan_i32", "agn_pool_sort_keys", "agn_pool_assign", "agn_pool_edge_candidates",
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
-            "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_collate",
+            "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce")
 
 
@@ -187,6 +187,11 @@ def lib():
             "agn_scatter_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
             "agn_wec_blocks": (i32, [i32]),
             "agn_edge_bwd_blocks": (i32, [i32]),
+            "agn_edge_features": (i32, [i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
+            "agn_normalize": (i32, [i32, i32, vp, i32, vp, vp, vp, i32, i32, vp]),
+            "agn_col_stats_temp_bytes": (C.c_size_t, [i32, i32]),
+            "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),
+            "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_wec_forward": (i32, [C.POINTER(WecArgs), vp]),

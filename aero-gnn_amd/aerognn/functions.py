@@ -173,22 +173,31 @@ def _ksegs(x, H):
 
 
 class MLPFn(torch.autograd.Function):
+    """models/mlp.py:40-51. `rows` (int64 / int32 [R] or None): the chain runs on x[rows] with the
+    gather done by the kernel's input loads (SEG_GATHER); the input gradient is then scattered
+    back with a fixed-order segment sum over the rows that read each input row."""
+
     @staticmethod
-    def forward(ctx, x, spec: ChainSpec, train, *params):
+    def forward(ctx, x, spec: ChainSpec, train, rows, *params):
         require_device(x)
         x = _c(x)
-        rows = x.shape[0]
+        nrow = x.shape[0] if rows is None else rows.numel()
         dt = x.dtype
-        out = torch.empty(rows, spec.out_dim, dtype=dt, device=x.device)
-        acts, hpre, stats = _alloc_saves(spec, rows, dt, x.device, train)
+        out = torch.empty(nrow, spec.out_dim, dtype=dt, device=x.device)
+        acts, hpre, stats = _alloc_saves(spec, nrow, dt, x.device, train)
         ks = _ksegs(x, spec.hidden)
         if len(ks) > L.MAX_SEG:
             raise NotImplementedError("aerognn MLP input wider than 3 x hidden")
-        segs = [(L.SEG_PLAIN, k, x.stride(0), x[:, k0:], None, None) for k0, k in ks]
-        mlp_forward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+        idx = None
+        if rows is not None:
+            idx = rows.to(torch.int32).contiguous()
+            segs = [(L.SEG_GATHER, k, x.stride(0), x[:, k0:], idx, None) for k0, k in ks]
+        else:
+            segs = [(L.SEG_PLAIN, k, x.stride(0), x[:, k0:], None, None) for k0, k in ks]
+        mlp_forward(rows=nrow, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
                     segs=segs, wpk=spec.wpk(), bias=spec.biases(), ln=spec.lnp(), out=out,
                     acts=acts, hpre=hpre, stats=stats)
-        ctx.spec = spec
+        ctx.spec, ctx.idx, ctx.nrow = spec, idx, nrow
         ctx.acts, ctx.hpre, ctx.stats = acts, hpre, stats
         ctx.save_for_backward(x)
         return out
@@ -198,23 +207,30 @@ class MLPFn(torch.autograd.Function):
         (x,) = ctx.saved_tensors
         spec = ctx.spec
         gy = _c(gy)
-        rows = x.shape[0]
+        rows = ctx.nrow
         dt = x.dtype
         gpre = _alloc_gpre(spec, rows, dt, x.device)
         ks = _ksegs(x, spec.hidden)
-        dparts = [torch.empty(rows, k, dtype=dt, device=x.device) if ctx.needs_input_grad[0] else None
-                  for _, k in ks]
+        need_dx = ctx.needs_input_grad[0]
+        dparts = [torch.empty(rows, k, dtype=dt, device=x.device) if need_dx else None for _, k in ks]
         nblk = bwd_nblocks(rows)
         part = torch.empty(nblk, 2 * spec.out_dim, dtype=torch.float32, device=x.device) if spec.ln else None
         nblk = mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
-                     in_dim=spec.in_dim, wtpk=spec.wtpk(), acts=ctx.acts or [], g=gy, gpre=gpre,
-                     ln_g=spec.lnp()[0] if spec.ln else None, hpre=ctx.hpre, stats=ctx.stats,
-                     din=[(k, d, False) for (_, k), d in zip(ks, dparts)], ln_partial=part)
+                            in_dim=spec.in_dim, wtpk=spec.wtpk(), acts=ctx.acts or [], g=gy, gpre=gpre,
+                            ln_g=spec.lnp()[0] if spec.ln else None, hpre=ctx.hpre, stats=ctx.stats,
+                            din=[(k, d, False) for (_, k), d in zip(ks, dparts)], ln_partial=part)
         dx = None
-        if ctx.needs_input_grad[0]:
+        if need_dx:
             dx = dparts[0] if len(dparts) == 1 else torch.cat(dparts, 1)
-        grads = _chain_param_grads(spec, gpre, x, ctx.acts, part, nblk)
-        return (dx, None, None, *grads)
+            if ctx.idx is not None:  # d x[r] = sum over the output rows i with rows[i] = r
+                from .graph import group_by
+                perm, rp = group_by(ctx.idx, x.shape[0])
+                dxs = torch.empty(x.shape[0], x.shape[1], dtype=dt, device=x.device)
+                segment_sum(x.shape[0], x.shape[1], rp, perm, dx, dxs)
+                dx = dxs
+        x0 = x if ctx.idx is None else x.index_select(0, ctx.idx.long())
+        grads = _chain_param_grads(spec, gpre, x0, ctx.acts, part, nblk)
+        return (dx, None, None, None, *grads)
 
 
 # --------------------------------------------------------------------------- GMP layer

@@ -131,28 +131,19 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
   return r;
 }
 
-// grid.x = sum over descs of nsplit_d * (output blocks of d): blockIdx.x -> (desc, split, block),
-// descs in order, each desc's blocks split-major. Splits per desc are in proportion to its rows
-// (agn_wgrad_plan), so a small (node-row) desc does not idle while a large (edge-row) one runs.
+// grid: x = row chunk (split), y = M block * nKb + K block, z = desc
 template <typename T>
-__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b) {
+__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
   __shared__ __attribute__((aligned(16))) T sx[DW_ROWS * LD];
-  int di = 0, local = blockIdx.x;
-  for (; di < b.n; ++di) {
-    const int nb = ((b.d[di].m + DW_BLK - 1) / DW_BLK) * ((b.d[di].k + DW_BLK - 1) / DW_BLK) * b.d[di].nsplit;
-    if (local < nb) break;
-    local -= nb;
-  }
-  if (di >= b.n) return;
-  const agn_wgrad_desc& d = b.d[di];
-  const int nsplit = d.nsplit;
+  const agn_wgrad_desc& d = b.d[blockIdx.z];
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK;
   const int nMb = (d.m + DW_BLK - 1) / DW_BLK;
-  const int split = local / (nMb * nKb), blk = local - split * (nMb * nKb);
-  const int mb = blk / nKb, kb = blk % nKb;
+  if ((int)blockIdx.y >= nMb * nKb) return;
+  const int mb = blockIdx.y / nKb, kb = blockIdx.y % nKb;
   const int m0 = mb * DW_BLK, k0 = kb * DW_BLK;
+  const int split = blockIdx.x;
   const int per = ((d.rows + nsplit - 1) / nsplit + DW_ROWS - 1) / DW_ROWS * DW_ROWS;
   const int rbeg = split * per, rend = min(d.rows, rbeg + per);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -385,8 +376,17 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
     maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
   }
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, dim3(total), dim3(DW_THREADS), 0, st, bb);
-  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, dim3(total), dim3(DW_THREADS), 0, st, bb);
+  // one split count for the whole batch (agn_wgrad_plan is uniform): grid (split, block, desc)
+  const int ns = bb.d[0].nsplit;
+  int maxblk = 1;
+  for (int i = 0; i < bb.n; ++i) {
+    if (bb.d[i].nsplit != ns) return AGN_E_ARG;
+    maxblk = out_blocks(bb.d[i]) > maxblk ? out_blocks(bb.d[i]) : maxblk;
+  }
+  (void)total;
+  dim3 grid(ns, maxblk, bb.n);
+  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, bb, ns);
+  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, bb, ns);
   else return AGN_E_DTYPE;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
   return launch_status();

@@ -145,7 +145,7 @@ AGN_DEV void load_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid,
 // ------------------------------------------------------------------------- forward
 // I/O modes of the general kernels (compile-time, chosen on the host per call):
 //   M_VEC : every input segment and the output are H wide (16-B row I/O everywhere)
-//   M_NIN : one PLAIN input of k <= 16 features (encoders: d_n = 6, d_e = 4), output H wide
+//   M_NIN : one PLAIN or GATHER input of k <= 16 features (encoders: d_n = 6, d_e = 4), output H wide
 //   M_NOUT: H-wide inputs, nlin > 1, output of <= 32 features, no LayerNorm (decoder: d_out = 4)
 //   M_GEN : anything else (masked 4-feature chunks)
 enum { M_VEC = 0, M_GEN = 1, M_NIN = 2, M_NOUT = 3 };
@@ -219,8 +219,9 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       const int nu = units_k<T>(a.seg[s].k);
       __syncthreads();
       stage_block(wl, a.wpk[0], ku0, grp * NT, otn0, unit, nu);
-      if constexpr (MODE == M_NIN) {
-        load_row_narrow<T, NR>(v, reinterpret_cast<const T*>(a.seg[s].ptr) + (size_t)rr * a.seg[s].ld, a.seg[s].k, h);
+      if constexpr (MODE == M_NIN) {  // PLAIN, or GATHER (the caller's row order permuted in the load)
+        const int src_row = a.seg[s].kind == AGN_SEG_GATHER ? a.seg[s].index[rr] : rr;
+        load_row_narrow<T, NR>(v, reinterpret_cast<const T*>(a.seg[s].ptr) + (size_t)src_row * a.seg[s].ld, a.seg[s].k, h);
       } else {
         bool staged = false;
         if constexpr (STAGE && IN_FULL) {
@@ -1139,7 +1140,9 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   int mode = M_GEN;
   if (fwd_ptrs_aligned(a)) {
     if (in_full && out_full) mode = M_VEC;
-    else if (out_full && a->nseg == 1 && a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k <= 16) mode = M_NIN;
+    else if (out_full && a->nseg == 1 && (a->seg[0].kind == AGN_SEG_PLAIN || a->seg[0].kind == AGN_SEG_GATHER) &&
+             a->seg[0].k <= 16)
+      mode = M_NIN;
     else if (in_full && a->nlin > 1 && a->out_dim <= 32 && !a->use_ln) mode = M_NOUT;
   }
   const bool vec = mode == M_VEC;

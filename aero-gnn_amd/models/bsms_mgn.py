@@ -186,7 +186,7 @@ class BiStridedMeshGraphNet(nn.Module):
         n = node_attr.size(0)
         level, pools = self._hierarchy(edge_index, batch, pos, n)
         node_hidden = self.node_encoder(node_attr)
-        edge_hidden = self.edge_encoder(edge_attr[level.perm])
+        edge_hidden = self.edge_encoder.forward_rows(edge_attr, level.perm)
         if self.dropout is not None:
             node_hidden = self.dropout(node_hidden)
             edge_hidden = self.dropout(edge_hidden)

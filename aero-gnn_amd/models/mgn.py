@@ -41,7 +41,7 @@ class MeshGraphNet(nn.Module):
     def forward(self, node_attr: torch.Tensor, edge_attr: torch.Tensor, edge_index: torch.Tensor) -> torch.Tensor:
         level = Level.from_edge_index(edge_index, node_attr.shape[0])
         node_hidden = self.node_encoder(node_attr)
-        edge_hidden = self.edge_encoder(edge_attr[level.perm])
+        edge_hidden = self.edge_encoder.forward_rows(edge_attr, level.perm)
         for layer in self.layers:
             node_hidden, edge_hidden = layer.forward_level(node_hidden, edge_hidden, level)
         return self.decoder(node_hidden)

@@ -53,4 +53,14 @@ class MLP(nn.Module):
             raise NotImplementedError("aerognn fused MLP: dropout > 0 in training is not implemented")
         s = self.spec()
         s.pack.update(x.dtype, x.device)
-        return MLPFn.apply(x, s, torch.is_grad_enabled(), *s.params())
+        return MLPFn.apply(x, s, torch.is_grad_enabled(), None, *s.params())
+
+    def forward_rows(self, x, rows):
+        """self.forward(x[rows]) with the row gather fused into the first layer's input loads (the
+        kernel reads row rows[i] for output row i; no gathered copy): the edge encoder on the
+        caller's edge features in a level's receiver-grouped order."""
+        if self.training and self.dropout.p > 0:
+            raise NotImplementedError("aerognn fused MLP: dropout > 0 in training is not implemented")
+        s = self.spec()
+        s.pack.update(x.dtype, x.device)
+        return MLPFn.apply(x, s, torch.is_grad_enabled(), rows, *s.params())

@@ -65,7 +65,7 @@ class poolMGN(nn.Module):
         g = BroadcastRowsFn.apply(g, groups)                          # [N, global_dim]
         x = self.node_encoder(torch.cat((node_attr, g), dim=-1))
         level = Level.from_edge_index(edge_index, n)
-        e = self.edge_encoder(edge_attr[level.perm])
+        e = self.edge_encoder.forward_rows(edge_attr, level.perm)
         for layer in self.layers:
             x, e = layer.forward_level(x, e, level)
         return self.decoder(x)

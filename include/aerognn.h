@@ -356,6 +356,24 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
  * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);
 
+/* ---- device data preparation (dataset.py:39-106, :358-409; train.py:50-51) ----
+ * agn_edge_features: out[i] = [pos[dst]-pos[src], |pos[dst]-pos[src]|] of edge e = perm ? perm[i] : i
+ *   (edge_index int64 [2][ne]), optionally normalised (v - mean) / std per column; [ne][pdim + 1] fp32.
+ * agn_normalize: out = (x - mean) / std per column (inverse: x * std + mean, denormalize_predictions).
+ * agn_col_stats: torch.std_mean(x, dim=0) (unbiased) of an [n][k] fp32 matrix, std clamped >= eps;
+ *   deterministic fp64 two-pass; scratch = agn_col_stats_temp_bytes(n, k).
+ * agn_collate: PyG Batch of B meshes concatenated row-wise: edge_index (in place) += the node offset
+ *   of each edge's mesh, batch[v] = mesh of node v; edge_off / node_off exclusive prefix sums [B + 1]. */
+int agn_edge_features(int ne, int pdim, const int64_t* edge_index, const float* pos, int pos_ld, const int64_t* perm,
+                      const float* mean, const float* std, float* out, void* stream);
+int agn_normalize(int n, int k, const float* x, int ld, const float* mean, const float* std, float* out, int out_ld,
+                  int inverse, void* stream);
+size_t agn_col_stats_temp_bytes(int n, int k);
+int agn_col_stats(int n, int k, const float* x, int ld, float* mean, float* std, float eps, void* scratch,
+                  void* stream);
+int agn_collate(int B, int64_t ne, int64_t nn, const int64_t* edge_off, const int64_t* node_off, int64_t* edge_index,
+                int64_t* batch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

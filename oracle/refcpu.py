@@ -249,3 +249,27 @@ def cfg_from_kwargs(**kw):
         global_pool_method=kw.get("global_pool_method", "mean"),
         n_hid_global_enc=kw.get("num_hidden_layers_global_encoder", 1),
     )
+
+
+# dataset.py:39-64 (compute_edge_attr)
+def compute_edge_attr(pos, edge_index):
+    source_pos = pos[edge_index[0]]
+    target_pos = pos[edge_index[1]]
+    edge_vec = target_pos - source_pos
+    edge_length = torch.norm(edge_vec, dim=1, keepdim=True)
+    return torch.cat([edge_vec, edge_length], dim=1)
+
+
+# dataset.py:358-392 (compute_normalization_stats)
+def compute_normalization_stats(xs, eas, ys):
+    x_std, x_mean = torch.std_mean(torch.vstack(xs), dim=0)
+    e_std, e_mean = torch.std_mean(torch.vstack(eas), dim=0)
+    y_std, y_mean = torch.std_mean(torch.vstack(ys), dim=0)
+    eps = 1e-8
+    return {"node_mean": x_mean, "node_std": torch.clamp(x_std, min=eps), "edge_mean": e_mean,
+            "edge_std": torch.clamp(e_std, min=eps), "target_mean": y_mean, "target_std": torch.clamp(y_std, min=eps)}
+
+
+# dataset.py:394-409 (normalize_data, one tensor)
+def normalize(v, mean, std):
+    return (v - mean) / std
