@@ -43,6 +43,9 @@ def compute_edge_attr(data=None, *, pos=None, edge_index=None, perm=None, stats=
     mean = std = None
     if stats is not None:
         mean, std = _f32(stats["edge_mean"]), _f32(stats["edge_std"])
+        require_device(mean, std)
+        if mean.numel() != p32.shape[1] + 1 or std.numel() != p32.shape[1] + 1:
+            raise ValueError("edge normalization stats must have pos_dim + 1 entries")
     check(L.lib().agn_edge_features(int(ne), int(p32.shape[1]), ptr(ei), ptr(p32), p32.stride(0),
                                     ptr(perm.contiguous() if perm is not None else None), ptr(mean), ptr(std),
                                     ptr(out), stream()), "edge_features")
@@ -92,6 +95,9 @@ def compute_normalization_stats(data_list):
 
 
 def _normalize(t, mean, std, inverse=False):
+    require_device(t, mean, std)  # statistics are read by the kernel: device tensors only
+    if mean.numel() != t.shape[1] or std.numel() != t.shape[1]:
+        raise ValueError(f"normalization stats of size {mean.numel()}/{std.numel()} for {t.shape[1]} columns")
     t32 = _f32(t)
     out = torch.empty_like(t32)
     check(L.lib().agn_normalize(t32.shape[0], t32.shape[1], ptr(t32), t32.stride(0), ptr(_f32(mean)), ptr(_f32(std)),

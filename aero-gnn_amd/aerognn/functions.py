@@ -456,17 +456,22 @@ class GMPFn(torch.autograd.Function):
                         segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
                         wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
             eb = spec.eb
+            # E-row (edge chain) and N-row (projection, node chain) weight gradients go to separate
+            # agn_wgrad launches: one split count serves all descs of a launch, and mixing 6x
+            # different row counts leaves most workgroups idle behind the edge descs (measured)
             wg = WGrad()
             if fused:
-                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)  # filled by wg.run()
-                wg.add(g0, e, dwe)
+                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
+                we = WGrad()
+                we.add(g0, e, dwe)
+                we.run()
                 eg = [dwe]
                 for l in range(3):
                     eg += [dW13[l], db13[l]]
                 eg = eg[:1] + [t if t.dtype == p.dtype else t.to(p.dtype) for t, p in zip(eg[1:], es.params()[1:7])]
                 eg += list(_ln_grads(part_e, nb_e, H, es.ln[0].dtype))
             else:
-                eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e, wg)
+                eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e)
             dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dbd = torch.empty(H, dtype=torch.float32, device=dev)
@@ -474,8 +479,8 @@ class GMPFn(torch.autograd.Function):
             wg.add(dPd, x, dwd, dbd)
             grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n, wg)
             wg.run()
-            if fused:
-                eg[0] = eg[0] if eg[0].dtype == es.linears[0][0].dtype else eg[0].to(es.linears[0][0].dtype)
+            if fused and eg[0].dtype != es.linears[0][0].dtype:
+                eg[0] = eg[0].to(es.linears[0][0].dtype)
             grads_edge = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
             return (dx, de, None, None, None, *grads_edge, *grads_node)
         else:

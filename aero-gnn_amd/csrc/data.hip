@@ -23,12 +23,12 @@ __global__ void edge_features_kernel(int ne, int pdim, const int64_t* __restrict
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   float acc = 0.f;
   for (int c = 0; c < pdim; ++c) {
-    v[c] = pos[d * pos_ld + c] - pos[s * pos_ld + c];
-    acc = c == 0 ? v[c] * v[c] : __builtin_fmaf(v[c], v[c], acc);
+    v[c] = __fsub_rn(pos[d * pos_ld + c], pos[s * pos_ld + c]);
+    acc = c == 0 ? __fmul_rn(v[c], v[c]) : __builtin_fmaf(v[c], v[c], acc);
   }
   v[pdim] = sqrtf(acc);
   float* o = out + (size_t)i * (pdim + 1);
-  for (int c = 0; c <= pdim; ++c) o[c] = mean ? (v[c] - mean[c]) / std[c] : v[c];
+  for (int c = 0; c <= pdim; ++c) o[c] = mean ? __fdiv_rn(__fsub_rn(v[c], mean[c]), std[c]) : v[c];
 }
 
 // out = (x - mean) / std per column, any row stride; in place allowed
@@ -38,7 +38,15 @@ __global__ void normalize_kernel(int n, int k, const float* __restrict__ x, int 
   if (t >= (long)n * k) return;
   const int r = (int)(t / k), c = (int)(t - (long)r * k);
   const float v = x[(size_t)r * ld + c];
-  out[(size_t)r * out_ld + c] = inverse ? v * std[c] + mean[c] : (v - mean[c]) / std[c];
+  float o;
+  if (inverse) {
+    // separately rounded multiply and add (no FMA contraction): torch's v * std + mean on the host
+#pragma clang fp contract(off)
+    o = v * std[c] + mean[c];
+  } else {
+    o = (v - mean[c]) / std[c];
+  }
+  out[(size_t)r * out_ld + c] = o;
 }
 
 // column statistics (torch.std_mean(x, dim=0), unbiased, dataset.py:371-373), deterministic:

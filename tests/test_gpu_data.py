@@ -61,12 +61,14 @@ def test_normalization_stats_and_apply():
         print(f"{k}: max |ours - torch| / std = {err:.2e}")
         assert err <= 2e-6, (k, err)
     raw = [(d.x.cpu(), d.edge_attr.cpu(), d.y.cpu()) for d in samples]
-    D.normalize_data(samples, ref | {})  # the reference's statistics: bit-exact application
+    D.normalize_data(samples, {k: v.to(DEV) for k, v in ref.items()})  # the reference's statistics: bit-exact
     for d, (x, e, y) in zip(samples, raw):
         assert torch.equal(d.x.cpu(), R.normalize(x, ref["node_mean"], ref["node_std"]))
         assert torch.equal(d.edge_attr.cpu(), R.normalize(e, ref["edge_mean"], ref["edge_std"]))
         assert torch.equal(d.y.cpu(), R.normalize(y, ref["target_mean"], ref["target_std"]))
     back = D.denormalize_predictions(samples[0].y, {k: v.to(DEV) for k, v in ref.items()}).cpu()
+    with pytest.raises(RuntimeError):  # host statistics are refused, not dereferenced by the kernel
+        D.denormalize_predictions(samples[0].y, ref)
     assert torch.equal(back, samples[0].y.cpu() * ref["target_std"] + ref["target_mean"])
 
 
