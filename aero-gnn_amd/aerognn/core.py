@@ -392,7 +392,14 @@ class WGrad:
                 if db is not None:
                     b.d[j].db_partial = ptr(scratch[o:o + bsz[j]])
                     o += bsz[j]
-            check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
+            # operator I/O: G and X read once per row (+ the fp32 dW / db written); its SURVEY §8(d)
+            # share is 0 (a fused backward keeps G in registers), so the alg_bytes slot carries 0
+            s_el = live[0][0].element_size()
+            io = sum(logical_rows(G) * (G.shape[1] + X.shape[1]) * s_el + 4 * G.shape[1] * (X.shape[1] + 1)
+                     for G, X, _, _ in live)
+            fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _ in live)
+            with timed("wgrad", (0.0, fl, io)):
+                check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
         self.items = []
 
 
