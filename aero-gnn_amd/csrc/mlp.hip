@@ -597,6 +597,14 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   const int ntiles = (a.rows + 31) / 32;
   const agn_seg& sg = a.seg[0];
   const ResTiles tw(ntiles, threadIdx.x >> 6);
+  // the sender / receiver ids of the wave's next tile are loaded one tile ahead, so a tile's
+  // projection-row gathers issue together with its e loads (one memory latency per tile, not two)
+  int nsrc = 0, ndst = 0;
+  if (a.proj && tw.first < tw.end) {
+    const int r0 = min(tw.first * 32 + c, a.rows - 1);
+    nsrc = a.src[r0];
+    ndst = a.dst[r0];
+  }
   for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
     const int row = tile * 32 + c;
@@ -605,9 +613,15 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     f32x16 acc[NT];
     BOp<T, NR> b;
     if (a.proj) {
+      const int cs = nsrc, cd = ndst;
+      if (tile + tw.step < tw.end) {
+        const int rn = min((tile + tw.step) * 32 + c, a.rows - 1);
+        nsrc = a.src[rn];
+        ndst = a.dst[rn];
+      }
       const T* P = reinterpret_cast<const T*>(a.proj);
-      const T* ps = P + (size_t)a.src[rr] * (2 * H);
-      const T* pd = P + (size_t)a.dst[rr] * (2 * H) + H;
+      const T* ps = P + (size_t)cs * (2 * H);
+      const T* pd = P + (size_t)cd * (2 * H) + H;
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) {
         float x[8], y[8];

@@ -148,11 +148,16 @@ class MeshGraphNetLayer(nn.Module):
         s = self.spec()
         s.pack.update(node_attr.dtype, node_attr.device)
         if _MEMLOG and not hasattr(self, '_edge_block_mem_logged'):
-            # the reference prints its EdgeBlock memory delta once per layer (mgnLayer.py:185-203)
+            # the reference prints its EdgeBlock memory deltas once per layer (mgnLayer.py:185-203).
+            # Here the edge and node blocks are one fused call, so the deltas cover both; the two
+            # device syncs run on this first call only (the reference syncs on every call).
+            torch.cuda.synchronize()
             before = torch.cuda.memory_allocated() / (1024 ** 2)
+            max_before = torch.cuda.max_memory_allocated() / (1024 ** 2)
             x, e = GMPFn.apply(node_attr, edge_attr, level, s, torch.is_grad_enabled(), *s.params())
+            torch.cuda.synchronize()
             print(f"EdgeBlock - Allocated: {torch.cuda.memory_allocated() / (1024 ** 2) - before:.2f} MB, "
-                  f"Peak increase: {0.0:.2f} MB")
+                  f"Peak increase: {torch.cuda.max_memory_allocated() / (1024 ** 2) - max_before:.2f} MB")
             self._edge_block_mem_logged = True
             return x, e
         return GMPFn.apply(node_attr, edge_attr, level, s, torch.is_grad_enabled(), *s.params())
