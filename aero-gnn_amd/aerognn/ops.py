@@ -11,6 +11,7 @@ torch.compile / FakeTensorMode, and autograd formulas that are themselves torch.
       out[r] = sum (or mean) of src[i] over index[i] == r, in increasing i (torch_scatter's CPU
       order; empty groups give 0). Grouping: agn_radix_sort_u64 + agn_row_ptr; sum:
       agn_segment_sum. Backward: gather_rows (mean: divided by the group size).
+  group_ptr(index [n], dim_size) -> int32 [dim_size + 1] group offsets (radix sort + agn_row_ptr).
   gather_rows(src [m,k], index [n], rowptr=None) -> [n, k]
       out[i] = src[index[i]] (/ group size of index[i] when rowptr is given): agn_gather_rows.
       Backward: scatter_sum.
@@ -56,6 +57,20 @@ def _rows2d(t: Tensor, what: str) -> Tensor:
     return t.contiguous()
 
 
+# ------------------------------------------------------------------------------- group_ptr
+@torch.library.custom_op("aerognn::group_ptr", mutates_args=())
+def group_ptr(index: Tensor, dim_size: int) -> Tensor:
+    """int32 [dim_size + 1] offsets of the groups of `index` (group sizes = diff): the count a
+    mean divides by, as a tensor op so autograd formulas stay traceable."""
+    require_device(index)
+    return _groups(index, dim_size)[1]
+
+
+@group_ptr.register_fake
+def _(index, dim_size):
+    return index.new_empty(dim_size + 1, dtype=I32)
+
+
 # ------------------------------------------------------------------------------- scatter_sum
 @torch.library.custom_op("aerognn::scatter_sum", mutates_args=())
 def scatter_sum(src: Tensor, index: Tensor, dim_size: int, mean: bool = False) -> Tensor:
@@ -84,9 +99,7 @@ def _scatter_sum_ctx(ctx, inputs, output):
 
 def _scatter_sum_bwd(ctx, g):
     (index,) = ctx.saved_tensors
-    rowptr = None
-    if ctx.mean:
-        _, rowptr = _groups(index, ctx.dim_size)
+    rowptr = torch.ops.aerognn.group_ptr(index, ctx.dim_size) if ctx.mean else None
     return torch.ops.aerognn.gather_rows(g, index, rowptr), None, None, None
 
 

@@ -4,7 +4,7 @@ numerics run on the GPU (tests/test_gpu_ops.py)."""
 import pytest
 import torch
 
-OPS = ("scatter_sum", "gather_rows", "scatter_max", "scatter_max_backward", "edge_features")
+OPS = ("scatter_sum", "gather_rows", "scatter_max", "scatter_max_backward", "edge_features", "group_ptr")
 
 
 def test_ops_registered_with_schema():
