@@ -291,7 +291,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the secondary C4 strong-scaling measurement")
     ap.add_argument("--cpu-plan", action="store_true", help="run BASELINE.md §3's full CPU plan and exit")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"),
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r2e_pmc_traffic.json"),
                     help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels")
     args = ap.parse_args()
     if args.cpu_plan:

@@ -4,6 +4,7 @@
 #   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), kernel trace only -> gpurun_out/pmc_{fetch,write}_$TAG
 #   3. tools/pmc_traffic.py -> gpurun_out/pmc_traffic_$TAG.json
 #   4. one MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE) -> mfma_$TAG.json
+#   5. one stall pass (wave cycles split into waiting / issue-blocked / issuing) -> sq_$TAG.json
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -e
 TAG=${1:-r2}
@@ -22,3 +23,8 @@ python tools/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG 
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d gpurun_out/pmc_mfma_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_mfma_$TAG.log 2>&1
 python tools/mfma_busy.py gpurun_out/pmc_mfma_$TAG gpurun_out/mfma_$TAG.json
+#   5. one stall pass (SQ_WAVE_CYCLES, SQ_ACTIVE_INST_ANY/VALU, SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_INSTS_VALU) -> sq_$TAG.json
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+    SQ_INSTS_VALU --output-format csv -d gpurun_out/pmc_sq_$TAG -o c3 -- python $B --steps 1 --warmup 1 \
+    > gpurun_out/pmc_sq_$TAG.log 2>&1
+python tools/sq_stall.py gpurun_out/pmc_sq_$TAG gpurun_out/sq_$TAG.json
