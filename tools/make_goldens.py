@@ -16,6 +16,9 @@ import os
 import sys
 import types
 
+# the reference tree is read-only input: never leave __pycache__ files in it when importing it
+sys.dont_write_bytecode = True
+
 import numpy as np
 import torch
 
