@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("AEROGNN_LIB") or os.path.join(_HERE, "libaerognn.so")
 
 MAX_LIN = 8
 MAX_SEG = 3
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
 OPT_RESIDENT = 0
 

@@ -60,7 +60,9 @@ def dt_code(dtype) -> int:
         return L.F32
     if dtype == torch.bfloat16:
         return L.BF16
-    raise NotImplementedError(f"aerognn kernels compute in float32 or bfloat16, got {dtype}")
+    if dtype == torch.float16:
+        return L.F16
+    raise NotImplementedError(f"aerognn kernels compute in float32, bfloat16 or float16, got {dtype}")
 
 
 def tiled_empty(rows, width, dtype, device):

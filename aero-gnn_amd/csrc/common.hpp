@@ -18,6 +18,10 @@
 typedef __bf16 bf16;
 typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16;
+typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+typedef f16 f16x4 __attribute__((ext_vector_type(4)));
+typedef f16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -25,14 +29,16 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace agn {
 
-enum { DT_F32 = 0, DT_BF16 = 1 };
+enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
 
 // ---------------------------------------------------------------- element access
 AGN_DEV float to_f(float v) { return v; }
 AGN_DEV float to_f(bf16 v) { return (float)v; }
+AGN_DEV float to_f(f16 v) { return (float)v; }
 template <typename T> AGN_DEV T from_f(float v);
 template <> AGN_DEV float from_f<float>(float v) { return v; }
 template <> AGN_DEV bf16 from_f<bf16>(float v) { return (bf16)v; }
+template <> AGN_DEV f16 from_f<f16>(float v) { return (f16)v; }
 
 // round-trip through storage type T (what a stored-then-reloaded value looks like)
 template <typename T> AGN_DEV float round_t(float v) { return to_f(from_f<T>(v)); }
@@ -42,7 +48,15 @@ AGN_DEV f32x4 load4(const bf16* p) {
   bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
   return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
 }
+AGN_DEV f32x4 load4(const f16* p) {
+  f16x4 v = *reinterpret_cast<const f16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
 AGN_DEV void store4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+AGN_DEV void store4(f16* p, f32x4 v) {
+  f16x4 b = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+  *reinterpret_cast<f16x4*>(p) = b;
+}
 AGN_DEV void store4(bf16* p, f32x4 v) {
   bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
   *reinterpret_cast<bf16x4*>(p) = b;
@@ -84,6 +98,16 @@ AGN_DEV void swap_halves(uint32_t& a, uint32_t& b) {
 AGN_DEV uint32_t pack2(float x, float y) { return __builtin_bit_cast(uint32_t, bf16x2{(bf16)x, (bf16)y}); }
 AGN_DEV float lo_bf16(uint32_t u) { return __uint_as_float(u << 16); }
 AGN_DEV float hi_bf16(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// the same for either 16-bit storage type (T = bf16 / f16; fp16 converts, bf16 shifts)
+template <typename T> AGN_DEV uint32_t pack2t(float x, float y);
+template <> AGN_DEV uint32_t pack2t<bf16>(float x, float y) { return pack2(x, y); }
+template <> AGN_DEV uint32_t pack2t<f16>(float x, float y) { return __builtin_bit_cast(uint32_t, f16x2{(f16)x, (f16)y}); }
+template <typename T> AGN_DEV float lo16(uint32_t u);
+template <typename T> AGN_DEV float hi16(uint32_t u);
+template <> AGN_DEV float lo16<bf16>(uint32_t u) { return lo_bf16(u); }
+template <> AGN_DEV float hi16<bf16>(uint32_t u) { return hi_bf16(u); }
+template <> AGN_DEV float lo16<f16>(uint32_t u) { return (float)__builtin_bit_cast(f16x2, u)[0]; }
+template <> AGN_DEV float hi16<f16>(uint32_t u) { return (float)__builtin_bit_cast(f16x2, u)[1]; }
 
 // o[0..3] = features 16i+4h.., o[4..7] = 16i+8+4h.. (acc registers 8i..8i+7)
 AGN_DEV void load8_w(float (&o)[8], const bf16* rowp, int i, int h) {
@@ -93,6 +117,14 @@ AGN_DEV void load8_w(float (&o)[8], const bf16* rowp, int i, int h) {
   swap_halves(a1, b1);
   o[0] = lo_bf16(a0); o[1] = hi_bf16(a0); o[2] = lo_bf16(a1); o[3] = hi_bf16(a1);
   o[4] = lo_bf16(b0); o[5] = hi_bf16(b0); o[6] = lo_bf16(b1); o[7] = hi_bf16(b1);
+}
+AGN_DEV void load8_w(float (&o)[8], const f16* rowp, int i, int h) {
+  const u32x4 x = *reinterpret_cast<const u32x4*>(rowp + 16 * i + 8 * h);
+  uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  o[0] = lo16<f16>(a0); o[1] = hi16<f16>(a0); o[2] = lo16<f16>(a1); o[3] = hi16<f16>(a1);
+  o[4] = lo16<f16>(b0); o[5] = hi16<f16>(b0); o[6] = lo16<f16>(b1); o[7] = hi16<f16>(b1);
 }
 AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
   const f32x4 x = load4(rowp + 16 * i + 4 * h), y = load4(rowp + 16 * i + 8 + 4 * h);
@@ -183,6 +215,13 @@ AGN_DEV void store8_w(bf16* rowp, int i, int h, const float (&v)[8], bool valid)
   swap_halves(a1, b1);
   if (valid) *reinterpret_cast<u32x4*>(rowp + 16 * i + 8 * h) = u32x4{a0, a1, b0, b1};
 }
+AGN_DEV void store8_w(f16* rowp, int i, int h, const float (&v)[8], bool valid) {
+  uint32_t a0 = pack2t<f16>(v[0], v[1]), a1 = pack2t<f16>(v[2], v[3]), b0 = pack2t<f16>(v[4], v[5]),
+           b1 = pack2t<f16>(v[6], v[7]);
+  swap_halves(a0, b0);
+  swap_halves(a1, b1);
+  if (valid) *reinterpret_cast<u32x4*>(rowp + 16 * i + 8 * h) = u32x4{a0, a1, b0, b1};
+}
 AGN_DEV void store8_w(float* rowp, int i, int h, const float (&v)[8], bool valid) {
   if (!valid) return;
   store4(rowp + 16 * i + 4 * h, f32x4{v[0], v[1], v[2], v[3]});
@@ -234,8 +273,8 @@ AGN_DEV void store_row_tiled(T* base, const float (&v)[NR], int row, int h, bool
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i)
       b[tiled_unit<T, NR>(row, i, h)] = __builtin_bit_cast(
-          uint4, u32x4{pack2(v[8 * i], v[8 * i + 1]), pack2(v[8 * i + 2], v[8 * i + 3]),
-                       pack2(v[8 * i + 4], v[8 * i + 5]), pack2(v[8 * i + 6], v[8 * i + 7])});
+          uint4, u32x4{pack2t<T>(v[8 * i], v[8 * i + 1]), pack2t<T>(v[8 * i + 2], v[8 * i + 3]),
+                       pack2t<T>(v[8 * i + 4], v[8 * i + 5]), pack2t<T>(v[8 * i + 6], v[8 * i + 7])});
   } else {
 #pragma unroll
     for (int i = 0; i < NR / 4; ++i)
@@ -250,7 +289,7 @@ AGN_DEV void load_row_tiled(float (&v)[NR], const T* base, int row, int h) {
     for (int i = 0; i < NR / 8; ++i) {
       const u32x4 x = __builtin_bit_cast(u32x4, b[tiled_unit<T, NR>(row, i, h)]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { v[8 * i + 2 * j] = lo_bf16(x[j]); v[8 * i + 2 * j + 1] = hi_bf16(x[j]); }
+      for (int j = 0; j < 4; ++j) { v[8 * i + 2 * j] = lo16<T>(x[j]); v[8 * i + 2 * j + 1] = hi16<T>(x[j]); }
     }
   } else {
 #pragma unroll
@@ -269,7 +308,7 @@ AGN_DEV void unpack8(float (&v)[8], uint4 u) {
 template <typename T, int NR>
 AGN_DEV f32x4 load4_tiled(const T* base, int q, int row, int h) {
   if constexpr (sizeof(T) == 2) {
-    const bf16* p = base + tiled_unit<T, NR>(row, q >> 1, h) * 8 + 4 * (q & 1);
+    const T* p = base + tiled_unit<T, NR>(row, q >> 1, h) * 8 + 4 * (q & 1);
     return load4(p);
   } else {
     return load4(base + tiled_unit<T, NR>(row, q, h) * 4);
@@ -287,7 +326,8 @@ AGN_DEV void store8_tiled(T* base, int i, int row, int h, const float (&v)[8], b
   uint4* b = reinterpret_cast<uint4*>(base);
   if constexpr (sizeof(T) == 2) {
     b[tiled_unit<T, NR>(row, i, h)] =
-        __builtin_bit_cast(uint4, u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])});
+        __builtin_bit_cast(uint4, u32x4{pack2t<T>(v[0], v[1]), pack2t<T>(v[2], v[3]), pack2t<T>(v[4], v[5]),
+                                        pack2t<T>(v[6], v[7])});
   } else {
     b[tiled_unit<T, NR>(row, 2 * i, h)] = __builtin_bit_cast(uint4, f32x4{v[0], v[1], v[2], v[3]});
     b[tiled_unit<T, NR>(row, 2 * i + 1, h)] = __builtin_bit_cast(uint4, f32x4{v[4], v[5], v[6], v[7]});
@@ -299,7 +339,7 @@ AGN_DEV void load8_tiled(float (&v)[8], const T* base, int i, int row, int h) {
   if constexpr (sizeof(T) == 2) {
     const u32x4 x = __builtin_bit_cast(u32x4, b[tiled_unit<T, NR>(row, i, h)]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { v[2 * j] = lo_bf16(x[j]); v[2 * j + 1] = hi_bf16(x[j]); }
+    for (int j = 0; j < 4; ++j) { v[2 * j] = lo16<T>(x[j]); v[2 * j + 1] = hi16<T>(x[j]); }
   } else {
     const f32x4 x = __builtin_bit_cast(f32x4, b[tiled_unit<T, NR>(row, 2 * i, h)]);
     const f32x4 y = __builtin_bit_cast(f32x4, b[tiled_unit<T, NR>(row, 2 * i + 1, h)]);
@@ -393,6 +433,47 @@ template <int NR> struct BOp<bf16, NR> {
     }
   }
 };
+template <int NR> struct BOp<f16, NR> {
+  static constexpr int RPU = 8;
+  f16x8 u[NR / 8];
+  AGN_DEV void set(const float (&v)[NR]) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[i][j] = (f16)v[8 * i + j];
+  }
+  AGN_DEV void mfma(f32x16& acc, const uint4& a_raw, int unit) const {
+    f16x8 a = *reinterpret_cast<const f16x8*>(&a_raw);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, u[unit], acc, 0, 0, 0);
+  }
+  template <int NT>
+  AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[i][j] = (f16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
+  }
+  AGN_DEV void get8(float (&o)[8], int i) const {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)u[i][j];
+  }
+  AGN_DEV void store_tiled(f16* base, int row, int h, bool valid) const {
+    if (!valid) return;
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i)
+      reinterpret_cast<uint4*>(base)[tiled_unit<f16, NR>(row, i, h)] = __builtin_bit_cast(uint4, u[i]);
+  }
+  AGN_DEV void store(f16* rowp, int h, bool valid) const {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      const u32x4 x = __builtin_bit_cast(u32x4, u[i]);
+      uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+      swap_halves(a0, b0);
+      swap_halves(a1, b1);
+      if (valid) *reinterpret_cast<u32x4*>(rowp + 16 * i + 8 * h) = u32x4{a0, a1, b0, b1};
+    }
+  }
+};
 template <int NR> struct BOp<float, NR> {
   static constexpr int RPU = 4;
   float u[NR];
@@ -443,6 +524,7 @@ template <int NR> AGN_DEV bool bop_pos(const BOp<bf16, NR>& b, int i) {
   const uint32_t w = __builtin_bit_cast(u32x4, b.u[i / 8])[(i % 8) / 2];
   return (int32_t)((i & 1) ? (w & 0xffff0000u) : (w << 16)) > 0;
 }
+template <int NR> AGN_DEV bool bop_pos(const BOp<f16, NR>& b, int i) { return (float)b.u[i / 8][i % 8] > 0.f; }
 template <int NR> AGN_DEV bool bop_pos(const BOp<float, NR>& b, int i) { return b.u[i] > 0.f; }
 template <typename T, int NR>
 AGN_DEV void store_relu_mask(void* base, const BOp<T, NR>& b, int tile, int lane) {

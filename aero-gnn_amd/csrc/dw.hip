@@ -12,6 +12,8 @@
 #include "common.hpp"
 #include "aerognn.h"
 
+#include <type_traits>
+
 using namespace agn;
 
 namespace {
@@ -27,6 +29,7 @@ template <typename T> struct DwTile;
 // LDS row stride in elements: bf16 136 (272 B, breaks the 4-row bank aliasing of tr reads),
 // f32 132 (528 B).
 template <> struct DwTile<bf16> { static constexpr int LD = 136; };
+template <> struct DwTile<f16> { static constexpr int LD = 136; };
 template <> struct DwTile<float> { static constexpr int LD = 132; };
 
 // One 64-row x 128-col stage of a row-major [rows][ld] matrix, moved global -> registers ->
@@ -186,7 +189,13 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) {
+            if constexpr (std::is_same<T, f16>::value)  // same fragments, fp16 products
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a[i]),
+                                                                 __builtin_bit_cast(f16x8, bb[j]), acc[i][j], 0, 0, 0);
+            else
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);
+          }
       }
     } else {
       const float* fg = reinterpret_cast<const float*>(sg);
@@ -386,6 +395,7 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   (void)total;
   dim3 grid(ns, maxblk, bb.n);
   if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, bb, ns);
+  else if (dtype == AGN_F16) hipLaunchKernelGGL(wgrad_kernel<f16>, grid, dim3(DW_THREADS), 0, st, bb, ns);
   else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, bb, ns);
   else return AGN_E_DTYPE;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);

@@ -25,7 +25,7 @@ AGN_DEV void load8(float (&o)[8], const T* row, int f0, int k, bool vec) {
     if constexpr (sizeof(T) == 2) {
       const u32x4 x = *reinterpret_cast<const u32x4*>(row + f0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { o[2 * i] = lo_bf16(x[i]); o[2 * i + 1] = hi_bf16(x[i]); }
+      for (int i = 0; i < 4; ++i) { o[2 * i] = lo16<T>(x[i]); o[2 * i + 1] = hi16<T>(x[i]); }
     } else {
       const f32x4 x = load4(row + f0), y = load4(row + f0 + 4);
 #pragma unroll
@@ -40,8 +40,8 @@ template <typename T>
 AGN_DEV void store8(T* row, int f0, int k, bool vec, const float (&v)[8]) {
   if (vec && f0 + 7 < k) {
     if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<u32x4*>(row + f0) = u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]),
-                                                  pack2(v[6], v[7])};
+      *reinterpret_cast<u32x4*>(row + f0) = u32x4{pack2t<T>(v[0], v[1]), pack2t<T>(v[2], v[3]),
+                                                  pack2t<T>(v[4], v[5]), pack2t<T>(v[6], v[7])};
     } else {
       store4(row + f0, f32x4{v[0], v[1], v[2], v[3]});
       store4(row + f0 + 4, f32x4{v[4], v[5], v[6], v[7]});
@@ -541,6 +541,7 @@ int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_
   hipStream_t st = (hipStream_t)stream;
   if (dtype == AGN_F32) return seg_sum_t<float>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
+  if (dtype == AGN_F16) return seg_sum_t<f16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   return AGN_E_DTYPE;
 }
 
@@ -557,6 +558,9 @@ int agn_segment_max(int rows, int k, int dtype, const int32_t* ptr, const int32_
   else if (dtype == AGN_BF16)
     hipLaunchKernelGGL(segment_max_kernel<bf16>, g, dim3(256), 0, st, rows, k, ptr, perm, (const bf16*)src, src_ld,
                        (bf16*)out, out_ld, argmax);
+  else if (dtype == AGN_F16)
+    hipLaunchKernelGGL(segment_max_kernel<f16>, g, dim3(256), 0, st, rows, k, ptr, perm, (const f16*)src, src_ld,
+                       (f16*)out, out_ld, argmax);
   else
     return AGN_E_DTYPE;
   const hipError_t e = hipGetLastError();
@@ -576,6 +580,9 @@ int agn_segment_max_backward(int rows, int k, int dtype, const int32_t* argmax, 
   else if (dtype == AGN_BF16)
     hipLaunchKernelGGL(segment_max_bwd_kernel<bf16>, g, dim3(256), 0, st, rows, k, argmax, (const bf16*)gout, gout_ld,
                        (bf16*)dx, dx_ld);
+  else if (dtype == AGN_F16)
+    hipLaunchKernelGGL(segment_max_bwd_kernel<f16>, g, dim3(256), 0, st, rows, k, argmax, (const f16*)gout, gout_ld,
+                       (f16*)dx, dx_ld);
   else
     return AGN_E_DTYPE;
   const hipError_t e = hipGetLastError();
@@ -589,6 +596,7 @@ int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* 
   hipStream_t st = (hipStream_t)stream;
   if (dtype == AGN_F32) return gather_t<float>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
   if (dtype == AGN_BF16) return gather_t<bf16>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
+  if (dtype == AGN_F16) return gather_t<f16>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
   return AGN_E_DTYPE;
 }
 

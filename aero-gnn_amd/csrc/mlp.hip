@@ -970,15 +970,24 @@ AGN_DEV void pack_one(const agn_pack_desc& d, int tid) {
   const int i = lane & 31, hh = lane >> 5;
   const int unit = tid >> 6;
   const int ot0 = d.row_off / 32;
-  if (d.dst_dtype == AGN_BF16) {
+  if (d.dst_dtype == AGN_BF16 || d.dst_dtype == AGN_F16) {
     const int KU = (d.cols + 15) / 16, KUT = (d.dst_cols + 15) / 16, ku0 = d.col_off / 16;
     if (unit >= OT * KU) return;
     const int ot = unit / KU, ku = unit % KU;
-    bf16x8 o;
+    const size_t at = ((size_t)(ot0 + ot) * KUT + ku0 + ku) * 64 + lane;
+    if (d.dst_dtype == AGN_BF16) {
+      bf16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      o[j] = (bf16)wat(w, d.ld, d.rows, d.cols, d.trans, 32 * ot + i, 16 * ku + 8 * (j >> 2) + 4 * hh + (j & 3));
-    reinterpret_cast<bf16x8*>(d.dst)[((size_t)(ot0 + ot) * KUT + ku0 + ku) * 64 + lane] = o;
+      for (int j = 0; j < 8; ++j)
+        o[j] = (bf16)wat(w, d.ld, d.rows, d.cols, d.trans, 32 * ot + i, 16 * ku + 8 * (j >> 2) + 4 * hh + (j & 3));
+      reinterpret_cast<bf16x8*>(d.dst)[at] = o;
+    } else {
+      f16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        o[j] = (f16)wat(w, d.ld, d.rows, d.cols, d.trans, 32 * ot + i, 16 * ku + 8 * (j >> 2) + 4 * hh + (j & 3));
+      reinterpret_cast<f16x8*>(d.dst)[at] = o;
+    }
   } else {
     const int KU = 2 * ((d.cols + 15) / 16), KUT = 2 * ((d.dst_cols + 15) / 16), ku0 = d.col_off / 8;
     if (unit >= OT * KU) return;
@@ -994,6 +1003,7 @@ __global__ void pack_kernel(const agn_pack_desc* __restrict__ descs) {
   const agn_pack_desc d = descs[blockIdx.y];
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (d.src_dtype == AGN_BF16) pack_one<bf16>(d, tid);
+  else if (d.src_dtype == AGN_F16) pack_one<f16>(d, tid);
   else pack_one<float>(d, tid);
 }
 
@@ -1040,6 +1050,11 @@ inline int launch_status() {
       if (a->hidden == 128) { MODES(bf16, 4) }                                \
       else if (a->hidden == 64) { MODES(bf16, 2) }                            \
       else if (a->hidden == 32) { MODES(bf16, 1) }                            \
+      else return AGN_E_HIDDEN;                                               \
+    } else if (a->dtype == AGN_F16) {                                         \
+      if (a->hidden == 128) { MODES(f16, 4) }                                 \
+      else if (a->hidden == 64) { MODES(f16, 2) }                             \
+      else if (a->hidden == 32) { MODES(f16, 1) }                             \
       else return AGN_E_HIDDEN;                                               \
     } else {                                                                  \
       return AGN_E_DTYPE;                                                     \
@@ -1111,7 +1126,7 @@ const char* agn_error_string(int code) {
   switch (code) {
     case 0: return "success";
     case AGN_E_ARG: return "invalid argument";
-    case AGN_E_DTYPE: return "unsupported dtype (f32 / bf16 only)";
+    case AGN_E_DTYPE: return "unsupported dtype (f32 / bf16 / f16)";
     case AGN_E_HIDDEN: return "unsupported hidden size (32, 64, 128)";
     case AGN_E_SHAPE: return "unsupported shape";
     default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";

@@ -36,7 +36,7 @@ extern "C" {
 #define AGN_MAX_LIN 8
 #define AGN_MAX_SEG 3
 
-enum { AGN_F32 = 0, AGN_BF16 = 1 };
+enum { AGN_F32 = 0, AGN_BF16 = 1, AGN_F16 = 2 };
 enum { AGN_SEG_PLAIN = 0, AGN_SEG_GATHER = 1, AGN_SEG_SUM = 2, AGN_SEG_MEAN = 3 };
 enum { AGN_E_ARG = -1, AGN_E_DTYPE = -2, AGN_E_HIDDEN = -3, AGN_E_SHAPE = -4 };
 
@@ -56,7 +56,7 @@ typedef struct {
 
 typedef struct {
   int rows;
-  int dtype;       /* activation storage dtype AGN_F32 / AGN_BF16 */
+  int dtype;       /* activation storage dtype AGN_F32 / AGN_BF16 / AGN_F16 */
   int hidden;      /* 32, 64 or 128 */
   int nlin;        /* Linear layers in the chain (1..AGN_MAX_LIN), ReLU between */
   int out_dim;     /* features of the last Linear */
@@ -289,7 +289,7 @@ int agn_scatter_rows(int rows, int k, int dtype, const int32_t* idx, const void*
  * agn_mlp_forward; edges are visited in the level's CSC order (sums in caller edge order). */
 typedef struct {
   int n, e;
-  int dtype;                 /* AGN_F32 / AGN_BF16 (x, pab, tx, weights, out, grads) */
+  int dtype;                 /* AGN_F32 / AGN_BF16 (x, pab, tx, weights, out, grads; no f16) */
   int out_dim;               /* 64 or 128 */
   int hid;                   /* edge-weight MLP hidden width: 64 */
   int pos_dim, pos_ld;       /* pos: fp32 [n][pos_ld], pos_dim <= 4 */

@@ -11,6 +11,8 @@ of the drop-in boundary.
 * bf16: the whole C3 architecture in bf16 vs the fp32 oracle (reported; SURVEY §8 does not gate
   it), and the reference's own bf16 mode (`model.to(torch.bfloat16)`: bf16 parameters) vs the
   reference's bf16 outputs in tests/golden/layer_bf16.npz.
+* fp16: the reference's fp16 mode (fp16 parameters) vs its own fp16 outputs
+  (tests/golden/layer_fp16_h{32,128}.npz), and fp16 activations through a BSMS model.
 * edge cases: empty U-Net blocks (layers_per_scale=0 / [0, 2]), mixed +0.0/-0.0 and NaN x in the
   pooling sort, grouped-but-unsorted and gapped `batch` ids (unique_consecutive semantics,
   bsms_mgn.py:231-238), the hierarchy cache on reordered same-topology meshes, and guard bytes
@@ -204,6 +206,61 @@ def test_reference_bf16_mode_layer():
     for n, prm in layer.named_parameters():
         assert prm.grad is not None and prm.grad.dtype == torch.bfloat16, n
         assert torch.isfinite(prm.grad.float()).all(), n
+
+
+# ------------------------------------------------------------------------------ fp16
+@pytest.mark.parametrize("H", [32, 128])
+def test_reference_fp16_mode_layer(H):
+    """The reference's fp16 mode (train.py:35-38: fp16 default dtype, fp16 parameters) against
+    its own fp16 outputs (tests/golden/layer_fp16_h*.npz) and its fp32 outputs. fp16 keeps 11
+    significant bits, so the bar is rel-L2 <= 5e-3; the backward runs and gives finite fp16
+    gradients."""
+    from models.mgnLayer import MeshGraphNetLayer
+    d, m = load(f"layer_fp16_h{H}")
+    layer = MeshGraphNetLayer(H, H, H, 2, 2, "relu", True, "add", True)
+    layer.load_state_dict(params(d))
+    layer = layer.to(DEV).to(torch.float16)
+    x = d["x"].to(DEV).half().requires_grad_(True)
+    e = d["e"].to(DEV).half().requires_grad_(True)
+    xo, eo = layer(x, e, d["edge_index"].to(DEV))
+    assert xo.dtype == torch.float16 and eo.dtype == torch.float16
+    for got, key in ((xo, "x_out_fp16"), (eo, "e_out_fp16"), (xo, "x_out"), (eo, "e_out")):
+        r = rel_l2(got.float().cpu(), d[key])
+        print(f"fp16-parameter layer H={H} vs {key}: rel-L2 {r:.2e}")
+        assert r <= 5e-3, (key, r)
+    (xo.float().square().sum() + eo.float().square().sum()).backward()
+    for n, prm in layer.named_parameters():
+        assert prm.grad is not None and prm.grad.dtype == torch.float16, n
+        assert torch.isfinite(prm.grad.float()).all(), n
+    assert torch.isfinite(x.grad.float()).all() and torch.isfinite(e.grad.float()).all()
+
+
+def test_bsms_fp16_activations_vs_fp32_oracle():
+    """fp16 activations with fp32 master weights through the whole BSMS-4 model (general
+    kernels; the resident kernels are bf16-only): forward vs the fp32 oracle, deterministic, and
+    a full backward with finite gradients."""
+    from models.bsms_mgn import BiStridedMeshGraphNet
+    from oracle import refcpu as R
+    t = _mesh(60, 40)
+    kw = _kw(S=3, P=6, H=128)
+    torch.manual_seed(0)
+    model = BiStridedMeshGraphNet(6, 4, 4, **kw).to(DEV)
+    args = (t["x"].to(DEV).half(), t["edge_attr"].to(DEV).half(), t["edge_index"].to(DEV))
+    with torch.no_grad():
+        p1 = model(*args, pos=t["pos"].to(DEV))
+        p2 = model(*args, pos=t["pos"].to(DEV))
+    assert p1.dtype == torch.float16 and torch.equal(p1, p2)
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        ref = R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], R.cfg_from_kwargs(**kw), None, t["pos"],
+                             stable=True)
+    r = rel_l2(p1.float().cpu(), ref)
+    print(f"BSMS-3 (6 layers, H=128) fp16 activations vs fp32 oracle: rel-L2 {r:.2e}")
+    assert r <= 1e-2
+    out = model(*args, pos=t["pos"].to(DEV))
+    torch.nn.functional.mse_loss(out.float(), t["y"].to(DEV)).backward()
+    for n, prm in model.named_parameters():
+        assert prm.grad is not None and torch.isfinite(prm.grad).all(), n
 
 
 # ------------------------------------------------------------------------------ edge cases

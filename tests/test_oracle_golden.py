@@ -84,6 +84,22 @@ def test_layer(name):
     _check_grads({k[2:]: v for k, v in p.items()}, d)
 
 
+@pytest.mark.parametrize("name", ["layer_bf16", "layer_fp16_h32", "layer_fp16_h128"])
+def test_layer_16bit_modes(name):
+    """The reference's bf16 / fp16 modes (train.py:30-38: 16-bit parameters and activations): the
+    oracle, run with the golden's parameters cast to that dtype, reproduces the reference's
+    16-bit outputs bitwise, and its fp32 outputs bitwise in fp32."""
+    d, m = load(name)
+    dt, suffix = (torch.bfloat16, "bf16") if name == "layer_bf16" else (torch.float16, "fp16")
+    p = {"L." + k: v for k, v in params(d).items()}
+    cfg = dict(do_concat_trick=m["trick"], n_hid_edge=m["n_hid"], n_hid_node=m["n_hid"], aggregation="add")
+    xo, eo = R.gmp_layer(p, "L", d["x"], d["e"], d["edge_index"], cfg)
+    assert torch.equal(xo, d["x_out"]) and torch.equal(eo, d["e_out"])
+    ph = {k: v.to(dt) for k, v in p.items()}
+    xh, eh = R.gmp_layer(ph, "L", d["x"].to(dt), d["e"].to(dt), d["edge_index"], cfg)
+    assert torch.equal(xh.float(), d[f"x_out_{suffix}"]) and torch.equal(eh.float(), d[f"e_out_{suffix}"])
+
+
 @pytest.mark.parametrize("name", ["mgn5_f32", "mgn5_f64"])
 def test_mgn(name):
     d, m = load(name)

@@ -298,6 +298,24 @@ def case_bf16():
          x_out=xo, e_out=eo, x_out_bf16=xb.float(), e_out_bf16=eb.float(), **sd(layer))
 
 
+def case_fp16():
+    """The reference's fp16 mode (train.py:35-38: default dtype float16, so fp16 parameters):
+    the same layer as case_bf16 cast with .half(), H = 32 and H = 128."""
+    for H in (32, 128):
+        torch.manual_seed(6)
+        t = mesh_tensors(12, 8)
+        layer = MeshGraphNetLayer(H, H, H, 2, 2, "relu", True, "add", True)
+        x = torch.randn(t["x"].shape[0], H)
+        e = torch.randn(t["edge_index"].shape[1], H)
+        xo, eo = layer(x, e, t["edge_index"])
+        lh = MeshGraphNetLayer(H, H, H, 2, 2, "relu", True, "add", True)
+        lh.load_state_dict(layer.state_dict())
+        lh = lh.to(torch.float16)
+        xh, eh = lh(x.half(), e.half(), t["edge_index"])
+        save(f"layer_fp16_h{H}", dict(H=H, n_hid=2, trick=True), x=x, e=e, edge_index=t["edge_index"],
+             x_out=xo, e_out=eo, x_out_fp16=xh.float(), e_out_fp16=eh.float(), **sd(layer))
+
+
 def case_poolmgn():
     """poolMGN (models/poolmgn.py) for each global pooling method on a 2-graph batch, H = 32."""
     for method in ("mean", "max", "add"):
@@ -339,3 +357,4 @@ if __name__ == "__main__":
     case_bsms("bsms_s1", 1, 4, [(12, 8, 0)])
     case_downsample()
     case_bf16()
+    case_fp16()
