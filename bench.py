@@ -403,7 +403,14 @@ def main():
     step = make_step(model, batches, extra)
     elapsed = timed_run(step, args.steps, args.warmup)
     step_s = elapsed / args.steps
-    value = eu_step * args.steps * ws / elapsed / 1e6
+    eu_all = eu_step * ws
+    if ws > 1:  # every rank's own hierarchy (its mesh seed differs): sum the counts, not rank 0's x N
+        t_eu = torch.tensor([float(eu_step)], dtype=torch.float64, device=dev)
+        if D._host_staged():
+            t_eu = t_eu.cpu()
+        torch.distributed.all_reduce(t_eu)
+        eu_all = int(t_eu.item())
+    value = eu_all * args.steps / elapsed / 1e6
 
     # instrumented pass (not part of `value`): HIP events around every libaerognn launch
     kernels, roof = {}, None
@@ -473,7 +480,8 @@ def main():
         "data": "synthetic ellipsoid aero surface mesh (aerognn.meshgen), random-init weights (seed 0)",
         "config": {"workload": workload, "model": MODEL_NAME if args.model == "bsms_mgn" else "BSMS_MeshGraphNet",
                    **{k: v for k, v in extra.items() if k != "multi"}, "mode": args.mode,
-                   "edge_updates_per_step_per_gpu": eu_step, "level_edges": Es,
+                   "edge_updates_per_step_per_gpu": eu_step, "edge_updates_per_step_all_ranks": eu_all,
+                   "level_edges": Es,
                    "global_batch": extra.get("global_batch_meshes", ws), "parallelism": f"dp{ws}"},
         "roofline": roof,
         "kernels": kernels,
@@ -485,7 +493,14 @@ def main():
         st4 = make_step(m4, b4, ex4)
         k4 = min(args.steps, 5)
         el4 = timed_run(st4, k4, 1)
-        out["c4_strong"] = {"value": round(eu4 * k4 * ws / el4 / 1e6, 2), "unit": "M edge-updates/s",
+        eu4_all = eu4 * ws
+        if ws > 1:
+            t4 = torch.tensor([float(eu4)], dtype=torch.float64, device=dev)
+            if D._host_staged():
+                t4 = t4.cpu()
+            torch.distributed.all_reduce(t4)
+            eu4_all = int(t4.item())
+        out["c4_strong"] = {"value": round(eu4_all * k4 / el4 / 1e6, 2), "unit": "M edge-updates/s",
                             "ms_per_step": round(1e3 * el4 / k4, 3), "steps": k4, "warmup": 1, "scaling": "strong",
                             "workload": wl4, "edge_updates_per_step_per_gpu": eu4,
                             "note": "BASELINE.json configs[3] / north_star's 1->8 scaling case (fixed global batch)"}
