@@ -12,20 +12,19 @@
 // back together with the saved activations (2 KB/edge). Here one persistent launch keeps dW1..dW3
 // in registers for its whole lifetime, so G1..G3 never reach HBM:
 //
-//  * one 512-thread block per CU (8 waves, 2 per SIMD); the block walks ROUNDS of 128 edges (four
-//    32-row tiles) in CSC order, XCD-grouped like the resident kernels;
-//  * wave w = (p, hw): p = w >> 1 picks the round's tile (rows 32p..32p+31), hw = w & 1 the output
-//    feature half (features 64hw..64hw+63) of every per-row GEMM, so a pair of waves shares a tile;
-//  * per layer step L = 3, 2, 1 the round's G_L and X_L (= a_L) sit in LDS as [128 rows][136] bf16
-//    images: the dW MFMAs read 8-row columns of both with ds_read_b64_tr_b16 (k = rows), the chain
-//    MFMA (rows on lanes, common.hpp) reads its B operand rows straight from the G image and W_L^T
-//    from a double-buffered LDS copy that the previous step prefetched with global_load_lds;
-//  * wave (p, hw) owns dW_L[64hw..64hw+63][32p..32p+31] for L = 1..3: 2 accumulator tiles per L,
-//    96 registers for the whole launch; its 16 dW MFMAs per step are balanced with its 16 chain
-//    MFMAs, so every wave does the same work between the two barriers of a step;
-//  * the LayerNorm backward runs per round on the pair's halves: row sums over 64 features per
-//    wave, exchanged through LDS; d gamma / d beta are butterfly-reduced per lane and summed per
-//    block at the end. db_L are column sums of the G_L images.
+//  * one 256-thread block per CU (4 waves, one per SIMD: 512 registers each); the block walks
+//    ROUNDS of 128 edges (four 32-row tiles, tile p on wave p) in CSC order, XCD-grouped like
+//    the resident kernels;
+//  * per layer step L = 3, 2, 1 the round's G_L and X_L (= a_L) sit in LDS as [128 rows][128]
+//    bf16 images (XOR-swizzled 8-byte units, see swz): the dW MFMAs read 8-row columns of both
+//    with ds_read_b64_tr_b16 (k = rows), the chain MFMA (rows on lanes, common.hpp) reads its B
+//    operand rows straight from the G image and W_L^T from a double-buffered LDS copy that the
+//    previous step prefetched with global_load_lds;
+//  * wave w owns dW_L[0..127][32w..32w+31] for L = 1..3: 4 accumulator tiles per L, 192
+//    registers for the whole launch; its 32 dW MFMAs per step match its 32 chain MFMAs;
+//  * the LayerNorm backward runs before this kernel (an LN-only agn_mlp_backward writes G3);
+//    db_L are column sums of the G_L images.
+// Measured: exact, but latency-bound at one wave per SIMD, so it is opt-in.
 // Partials per block go to slabs summed in fixed order by agn_wgrad_reduce / agn_colsum: no atomics.
 #include "common.hpp"
 #include "aerognn.h"
