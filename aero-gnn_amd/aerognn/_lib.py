@@ -99,7 +99,8 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
-            "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce")
+            "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
+            "agn_proj_forward", "agn_proj_backward")
 
 
 class AeroGNNError(RuntimeError):
@@ -194,6 +195,8 @@ def lib():
             "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
+            "agn_proj_forward": (i32, [i32, vp, i32, vp, vp, vp, i32, vp]),
+            "agn_proj_backward": (i32, [i32, vp, vp, i32, vp, vp, i32, vp]),
             "agn_wec_forward": (i32, [C.POINTER(WecArgs), vp]),
             "agn_wec_backward": (i32, [C.POINTER(WecArgs), vp]),
         }

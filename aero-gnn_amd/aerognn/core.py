@@ -222,6 +222,27 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
         check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
 
 
+# The persistent projection kernels (csrc/proj.hip) for the sum-trick edge block's node-row
+# GEMMs; bitwise identical to the general-kernel path, which AEROGNN_PROJ_KERNEL=0 selects.
+def proj_kernel_ok(x, H):
+    import os
+    return (os.environ.get("AEROGNN_PROJ_KERNEL", "1") != "0" and x.dtype == torch.bfloat16 and H == 128
+            and x.dim() == 2 and x.shape[1] == 128 and x.stride(1) == 1)
+
+
+def proj_forward(rows, x, wpk, bias, out, tag=None, cost=None):
+    with timed(tag, cost):
+        check(L.lib().agn_proj_forward(rows, ptr(x), x.stride(0), wpk, bias, ptr(out), out.stride(0), stream()),
+              "proj_forward")
+
+
+def proj_backward(rows, dps, dpd, wtpk, dx, tag=None, cost=None):
+    assert dps.stride(0) == dpd.stride(0)
+    with timed(tag, cost):
+        check(L.lib().agn_proj_backward(rows, ptr(dps), ptr(dpd), dps.stride(0), wtpk, ptr(dx), dx.stride(0),
+                                        stream()), "proj_backward")
+
+
 def bwd_nblocks(rows):
     return int(L.lib().agn_mlp_bwd_nwaves(int(rows)))
 

@@ -21,7 +21,8 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_bwd_ok, bwd_nblocks, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
+from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_bwd_ok, bwd_nblocks,
+                   proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_max, segment_max_backward, segment_sum, stream)
@@ -353,10 +354,14 @@ class GMPFn(torch.autograd.Function):
         if spec.trick:
             P = torch.empty(N, 2 * H, dtype=dt, device=dev)
             sz = x.element_size()
-            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
-                        segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
-                        wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
-                        tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
+            if proj_kernel_ok(x, H):
+                proj_forward(N, x, spec.pack["proj"], spec.pack["proj_b"], P,
+                             tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
+            else:
+                mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=2 * H,
+                            segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
+                            wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
+                            tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
             mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
@@ -452,9 +457,14 @@ class GMPFn(torch.autograd.Function):
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
             dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
             dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
-            mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
-                        segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
-                        wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
+            if proj_kernel_ok(dx, H):
+                s_el = dx.element_size()
+                proj_backward(N, dPs, dPd, spec.pack["projT"], dx, tag="proj_bwd",
+                              cost=with_alg(alg8d_node(N, H, s_el, bwd=True), (4 * N * H * s_el, 4.0 * N * H * H)))
+            else:
+                mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
+                            segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
+                            wpk=[spec.pack["projT"]], bias=[None], resid=dx, out=dx)
             eb = spec.eb
             # E-row (edge chain) and N-row (projection, node chain) weight gradients go to separate
             # agn_wgrad launches: one split count serves all descs of a launch, and mixing 6x

@@ -356,6 +356,17 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
  * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);
 
+/* Node-row projections of the sum-trick edge block (mgnLayer.py:72-105, EdgeBlockSum's
+ * src_lin / dst_lin applied per node instead of per edge), bf16, H = 128, persistent with the
+ * packed weights resident in LDS (agn_pack layout, 64 KB):
+ *   agn_proj_forward : out[r][0:256] = x[r] . [W_s; W_d]^T + bias   (wpk: 256 x 128 packed)
+ *   agn_proj_backward: dx[r] += dps[r] . W_s + dpd[r] . W_d          (wtpk: 128 x 256 packed)
+ * Bitwise identical to agn_mlp_forward with nlin = 1 on the same operands. Rows 16-B aligned. */
+int agn_proj_forward(int rows, const void* x, int x_ld, const void* wpk, const float* bias, void* out, int out_ld,
+                     void* stream);
+int agn_proj_backward(int rows, const void* dps, const void* dpd, int dp_ld, const void* wtpk, void* dx, int dx_ld,
+                      void* stream);
+
 /* ---- device data preparation (dataset.py:39-106, :358-409; train.py:50-51) ----
  * agn_edge_features: out[i] = [pos[dst]-pos[src], |pos[dst]-pos[src]|] of edge e = perm ? perm[i] : i
  *   (edge_index int64 [2][ne]), optionally normalised (v - mean) / std per column; [ne][pdim + 1] fp32.

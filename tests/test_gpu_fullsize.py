@@ -73,6 +73,33 @@ def test_resident_kernels_bitwise_equal_general():
     assert worst <= 1e-6
 
 
+@pytest.mark.parametrize("nu,nv", [(150, 110), (97, 61)])  # 16,500 nodes; 5,917 nodes (ragged tile)
+def test_proj_kernels_bitwise_equal_general(nu, nv, monkeypatch):
+    """agn_proj_forward / agn_proj_backward (csrc/proj.hip, the node-row projections of the
+    sum-trick edge block) against the general MLP kernel they replace (AEROGNN_PROJ_KERNEL=0):
+    every output and gradient of a bf16 layer training step bitwise equal."""
+    from aerognn.graph import Level
+    from models.mgnLayer import MeshGraphNetLayer
+    m = _mesh(nu, nv)
+    ei = m["edge_index"].to(DEV)
+    N, E = m["x"].shape[0], ei.shape[1]
+    torch.manual_seed(0)
+    layer = MeshGraphNetLayer(128, 128, 128, 2, 2, do_concat_trick=True).to(DEV)
+    lv = Level.from_edge_index(ei, N)
+    g = torch.Generator(device="cpu").manual_seed(2)
+    x = torch.randn(N, 128, generator=g).to(DEV, torch.bfloat16)
+    e = torch.randn(E, 128, generator=g).to(DEV, torch.bfloat16)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("AEROGNN_PROJ_KERNEL", flag)
+        runs.append(_layer_step(layer, x, e, lv))
+    a, b = runs
+    for name, u, v in zip(("x'", "e'", "dx", "de"), a[:4], b[:4]):
+        assert torch.equal(u, v), name
+    for n in a[4]:
+        assert torch.equal(a[4][n], b[4][n]), n
+
+
 def test_resident_encoder_backward_bitwise_equal_general():
     """The edge encoder (MLP 4 -> 128, n_hid=2, LN; no input gradient) takes the resident
     backward too: gpre / parameter grads match the general kernel."""
