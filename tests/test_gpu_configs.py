@@ -317,6 +317,30 @@ def test_mgn_isolated_nodes_and_edgeless_graph(case):
         assert prm.grad is not None and torch.isfinite(prm.grad).all(), n
 
 
+def test_bsms_batch_with_tiny_meshes():
+    """Meshes of 6 and 12 nodes beside a normal one in one batch, 4 levels: the tiny graphs pool
+    down to a single node (and no edges) before the bottom; forward vs the oracle at 1e-5 and a
+    full backward."""
+    from aerognn.meshgen import collate, ellipsoid
+    from models.bsms_mgn import BiStridedMeshGraphNet
+    from oracle import refcpu as R
+    t = {k: torch.from_numpy(v) for k, v in collate([ellipsoid(3, 2, seed=0), ellipsoid(16, 10, seed=1),
+                                                      ellipsoid(4, 3, seed=2)]).items()}
+    kw = _kw(S=4, P=7, H=32)
+    torch.manual_seed(0)
+    model = BiStridedMeshGraphNet(6, 4, 4, **kw).to(DEV)
+    pred = model(t["x"].to(DEV), t["edge_attr"].to(DEV), t["edge_index"].to(DEV), batch=t["batch"].to(DEV),
+                 pos=t["pos"].to(DEV))
+    p = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        ref = R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], R.cfg_from_kwargs(**kw), t["batch"],
+                             t["pos"], stable=True)
+    _gate(pred, ref, what="BSMS-4 tiny meshes")
+    torch.nn.functional.mse_loss(pred, t["y"].to(DEV)).backward()
+    for n, prm in model.named_parameters():
+        assert prm.grad is not None and torch.isfinite(prm.grad).all(), n
+
+
 def test_signed_zero_and_nan_x_pool_like_torch_argsort():
     """-0.0 and +0.0 compare equal in torch.argsort (stable tie rule: node id decides) and NaN
     sorts last: the pooling keys follow."""
