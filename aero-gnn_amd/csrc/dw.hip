@@ -158,7 +158,11 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-  float bsum = 0.f;  // bias colsum partial (threads 0..127 own columns m0 + tid)
+  // bias colsum partial: thread t owns column m0 + (t & 127) over rows 16q..16q+15 of each stage
+  // (q = t >> 7 picks the even / odd 16-row groups), so all four waves share the walk; the two
+  // halves are added in a fixed order at the end
+  float bsum = 0.f;
+  __shared__ float bhalf[DW_BLK];
   StageRegs<T> rg, rx;
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
@@ -173,9 +177,12 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
       rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled);
     }
-    if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK) {
+    if (d.db_partial && kb == 0) {
+      const int col = threadIdx.x & (DW_BLK - 1), q = threadIdx.x >> 7;
+#pragma unroll
+      for (int gq = 0; gq < DW_ROWS / 32; ++gq)
 #pragma unroll 8
-      for (int r = 0; r < DW_ROWS; ++r) bsum += to_f(sg[r * LD + threadIdx.x]);
+        for (int r = 0; r < 16; ++r) bsum += to_f(sg[(32 * gq + 16 * q + r) * LD + col]);
     }
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -228,8 +235,12 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
         const int k = k0 + wk + 32 * j + (lane & 31);
         P[(size_t)m * kpad + k] = acc[i][j][r];
       }
-  if (d.db_partial && kb == 0 && threadIdx.x < DW_BLK)
-    d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum;
+  if (d.db_partial && kb == 0) {
+    __syncthreads();
+    if (threadIdx.x >= DW_BLK) bhalf[threadIdx.x - DW_BLK] = bsum;
+    __syncthreads();
+    if (threadIdx.x < DW_BLK) d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum + bhalf[threadIdx.x];
+  }
 }
 
 // out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns 64 column quads (256
