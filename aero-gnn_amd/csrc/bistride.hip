@@ -410,6 +410,10 @@ __global__ __launch_bounds__(256) void wec_bwd_src_kernel(const agn_wec_args a) 
       if (a->out_dim == 128) hipLaunchKernelGGL((KERNEL<bf16, 128>), GRID, dim3(256), 0, st, *a);    \
       else if (a->out_dim == 64) hipLaunchKernelGGL((KERNEL<bf16, 64>), GRID, dim3(256), 0, st, *a);  \
       else return AGN_E_SHAPE;                                                                       \
+    } else if (a->dtype == AGN_F16) {                                                                \
+      if (a->out_dim == 128) hipLaunchKernelGGL((KERNEL<f16, 128>), GRID, dim3(256), 0, st, *a);     \
+      else if (a->out_dim == 64) hipLaunchKernelGGL((KERNEL<f16, 64>), GRID, dim3(256), 0, st, *a);   \
+      else return AGN_E_SHAPE;                                                                       \
     } else {                                                                                         \
       return AGN_E_DTYPE;                                                                            \
     }                                                                                                \
@@ -544,6 +548,9 @@ int agn_scatter_rows(int rows, int k, int dtype, const int32_t* idx, const void*
   else if (dtype == AGN_BF16)
     hipLaunchKernelGGL(scatter_rows_kernel<bf16>, g, dim3(256), 0, st, rows, k, idx, (const bf16*)src, src_ld,
                        (bf16*)out, out_ld);
+  else if (dtype == AGN_F16)
+    hipLaunchKernelGGL(scatter_rows_kernel<f16>, g, dim3(256), 0, st, rows, k, idx, (const f16*)src, src_ld,
+                       (f16*)out, out_ld);
   else
     return AGN_E_DTYPE;
   return launch_status();

@@ -289,7 +289,7 @@ int agn_scatter_rows(int rows, int k, int dtype, const int32_t* idx, const void*
  * agn_mlp_forward; edges are visited in the level's CSC order (sums in caller edge order). */
 typedef struct {
   int n, e;
-  int dtype;                 /* AGN_F32 / AGN_BF16 (x, pab, tx, weights, out, grads; no f16) */
+  int dtype;                 /* AGN_F32 / AGN_BF16 / AGN_F16 (x, pab, tx, weights, out, grads) */
   int out_dim;               /* 64 or 128 */
   int hid;                   /* edge-weight MLP hidden width: 64 */
   int pos_dim, pos_ld;       /* pos: fp32 [n][pos_ld], pos_dim <= 4 */

@@ -208,7 +208,8 @@ def test_bsms_gnn_model_vs_oracle():
     assert np.median(errs) <= 1e-5 and errs.max() <= 1e-2, (np.median(errs), errs.max())
 
 
-def test_bsms_gnn_bf16_runs():
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_bsms_gnn_16bit_runs(dtype):
     from models.bsms_mgn import BSMS_MeshGraphNet, MultiScaleGraphPreprocessor
 
     class D:
@@ -221,6 +222,11 @@ def test_bsms_gnn_bf16_runs():
     model = BSMS_MeshGraphNet(6, 4, 4, num_levels=2, pos_dim=3).to(DEV)
     x, ea = m["x"].to(DEV), m["edge_attr"].to(DEV)
     p32 = model(x, ea, d.edge_index, multi_data=multi)
-    p16 = model(x.bfloat16(), ea.bfloat16(), d.edge_index, multi_data=multi)
-    assert torch.isfinite(p16.float()).all()
-    assert rel_l2(p16.float().detach().cpu(), p32.detach().cpu().double()) <= 5e-2
+    p16 = model(x.to(dtype), ea.to(dtype), d.edge_index, multi_data=multi)
+    assert p16.dtype == dtype and torch.isfinite(p16.float()).all()
+    r = rel_l2(p16.float().detach().cpu(), p32.detach().cpu().double())
+    print(f"BSMS-GNN {dtype}: rel-L2 {r:.2e} vs its fp32 run")
+    assert r <= (5e-2 if dtype == torch.bfloat16 else 1e-2)
+    p16.float().square().mean().backward()
+    for n, prm in model.named_parameters():
+        assert prm.grad is None or torch.isfinite(prm.grad).all(), n
