@@ -456,10 +456,36 @@ __global__ __launch_bounds__(256) void pool_cand_sort_kernel(int nc, const int32
                                                              const int64_t* __restrict__ refkey,
                                                              const int32_t* __restrict__ f2c,
                                                              int32_t* __restrict__ sorted) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // the wave's candidate keys are staged in LDS once (the O(d^2) rank loop then reads LDS
+  // broadcasts instead of three dependent global loads per comparison); larger lists fall back
+  constexpr int CAP = 256;
+  __shared__ int sk[4][CAP];
+  __shared__ int64_t sr[4][CAP];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 4 + w;
   if (c >= nc) return;
   const int b = cand_ptr[c], d = cand_ptr[c + 1] - b;
+  if (d <= CAP) {
+    for (int i = lane; i < d; i += 64) {
+      const int ei = cand[b + i];
+      sk[w][i] = f2c[src[ei]];
+      sr[w][i] = refkey[ei];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    for (int i = lane; i < d; i += 64) {
+      const int ki = sk[w][i];
+      const int64_t ri = sr[w][i];
+      int rank = 0;
+      for (int j = 0; j < d; ++j) {
+        const int kj = sk[w][j];
+        rank += (kj < ki) || (kj == ki && sr[w][j] < ri);
+      }
+      sorted[b + rank] = cand[b + i];
+    }
+    return;
+  }
   for (int i = lane; i < d; i += 64) {
     const int ei = cand[b + i];
     const int ki = f2c[src[ei]];
