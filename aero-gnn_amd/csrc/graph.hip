@@ -500,41 +500,61 @@ __global__ __launch_bounds__(256) void pool_cand_sort_kernel(int nc, const int32
   }
 }
 
+// distinct coarse senders per coarse node (one wave per node, as pool_emit_kernel)
 __global__ void pool_uniq_kernel(int nc, const int32_t* __restrict__ cand_ptr, const int32_t* __restrict__ sorted,
                                  const int32_t* __restrict__ src, const int32_t* __restrict__ f2c,
                                  int32_t* __restrict__ uniq) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= nc) return;
+  const int b = cand_ptr[c], end = cand_ptr[c + 1];
   int u = 0, prev = -1;
-  for (int p = cand_ptr[c]; p < cand_ptr[c + 1]; ++p) {
-    const int k = f2c[src[sorted[p]]];
-    u += (k != prev);
-    prev = k;
+  for (int p0 = b; p0 < end; p0 += 64) {
+    const int p = p0 + lane;
+    const bool in = p < end;
+    const int sv = in ? f2c[src[sorted[p]]] : -1;
+    int before = __shfl_up(sv, 1, 64);
+    if (lane == 0) before = prev;
+    u += __popcll(__ballot(in && sv != before));
+    prev = __shfl(sv, min(63, end - 1 - p0), 64);
   }
-  uniq[c] = u;
+  if (lane == 0) uniq[c] = u;
 }
 
+// One wave per coarse node c: its sorted candidates are processed 64 at a time; a candidate
+// opens a new coarse edge where its coarse sender differs from its predecessor's, and the coarse
+// edge index is crowptr[c] - 1 + the running count of openings (wave ballot + popcount): the same
+// output as the sequential walk, without its chain of dependent loads per candidate.
 __global__ void pool_emit_kernel(int nc, const int32_t* __restrict__ cand_ptr, const int32_t* __restrict__ sorted,
                                  const int32_t* __restrict__ src, const int32_t* __restrict__ f2c,
                                  const int32_t* __restrict__ crowptr, int32_t* __restrict__ csrc,
                                  int32_t* __restrict__ cdst, int32_t* __restrict__ cmem_ptr,
                                  int32_t* __restrict__ inv, int64_t* __restrict__ crefkey, int e_fine) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c > nc) return;
-  if (c == nc) { cmem_ptr[crowptr[nc]] = e_fine; return; }
-  int k = crowptr[c] - 1, prev = -1;
-  for (int p = cand_ptr[c]; p < cand_ptr[c + 1]; ++p) {
-    const int e = sorted[p];
-    const int s = f2c[src[e]];
-    if (s != prev) {
-      ++k;
-      csrc[k] = s;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) cmem_ptr[crowptr[nc]] = e_fine;
+  if (c >= nc) return;
+  const int b = cand_ptr[c], end = cand_ptr[c + 1];
+  int base = crowptr[c] - 1, prev = -1;  // index of the last opened coarse edge; its sender
+  for (int p0 = b; p0 < end; p0 += 64) {
+    const int p = p0 + lane;
+    const bool in = p < end;
+    const int e = in ? sorted[p] : 0;
+    const int sv = in ? f2c[src[e]] : -1;
+    int before = __shfl_up(sv, 1, 64);
+    if (lane == 0) before = prev;
+    const bool open = in && sv != before;
+    const uint64_t m = __ballot(open);
+    const int k = base + __popcll(m & ((2ull << lane) - 1ull));  // lane 63: all bits
+    if (open) {
+      csrc[k] = sv;
       cdst[k] = c;
       cmem_ptr[k] = p;
-      crefkey[k] = (int64_t)s * nc + c;
-      prev = s;
+      crefkey[k] = (int64_t)sv * nc + c;
     }
-    inv[e] = k;
+    if (in) inv[e] = k;
+    base += __popcll(m);
+    prev = __shfl(sv, min(63, end - 1 - p0), 64);
   }
 }
 
@@ -728,7 +748,7 @@ int agn_pool_edge_sort(int nc, const int32_t* c2f, const int32_t* c2f_ptr, const
   hipLaunchKernelGGL(pool_cand_list_kernel, g1(nc), dim3(256), 0, st, nc, c2f, c2f_ptr, rowptr, cand_ptr, cand_tmp);
   hipLaunchKernelGGL(pool_cand_sort_kernel, dim3((nc + 3) / 4), dim3(256), 0, st, nc, cand_ptr, cand_tmp, src, refkey,
                      f2c, cand_sorted);
-  hipLaunchKernelGGL(pool_uniq_kernel, g1(nc), dim3(256), 0, st, nc, cand_ptr, cand_sorted, src, f2c, uniq);
+  hipLaunchKernelGGL(pool_uniq_kernel, dim3((nc + 3) / 4), dim3(256), 0, st, nc, cand_ptr, cand_sorted, src, f2c, uniq);
   return launch_status();
 }
 
@@ -736,8 +756,8 @@ int agn_pool_edge_emit(int nc, const int32_t* cand_ptr, const int32_t* cand_sort
                        const int32_t* f2c, const int32_t* crowptr, int32_t* csrc, int32_t* cdst, int32_t* cmem_ptr,
                        int32_t* inv, int64_t* crefkey, int e_fine, void* stream) {
   if (nc < 0) return AGN_E_ARG;
-  hipLaunchKernelGGL(pool_emit_kernel, g1(nc + 1), dim3(256), 0, (hipStream_t)stream, nc, cand_ptr, cand_sorted, src,
-                     f2c, crowptr, csrc, cdst, cmem_ptr, inv, crefkey, e_fine);
+  hipLaunchKernelGGL(pool_emit_kernel, dim3(nc > 0 ? (nc + 3) / 4 : 1), dim3(256), 0, (hipStream_t)stream, nc,
+                     cand_ptr, cand_sorted, src, f2c, crowptr, csrc, cdst, cmem_ptr, inv, crefkey, e_fine);
   return launch_status();
 }
 
