@@ -300,19 +300,25 @@ __global__ __launch_bounds__(RS_THREADS) void rs_scatter_kernel(const uint64_t* 
   base[t] = offsets[(size_t)t * nblocks + blockIdx.x];
   const int tile0 = blockIdx.x * RS_TILE;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  // all of the thread's items are loaded up front (their latencies overlap), then ranked round
+  // by round in the same order as before
+  uint64_t kk[RS_ITEMS];
+  int32_t vv[RS_ITEMS];
+#pragma unroll
+  for (int i = 0; i < RS_ITEMS; ++i) {
+    const int p = tile0 + i * RS_THREADS + t;
+    kk[i] = p < n ? keys_in[p] : 0ull;
+    vv[i] = p < n ? vals_in[p] : 0;
+  }
+#pragma unroll
   for (int i = 0; i < RS_ITEMS; ++i) {
     for (int wv = 0; wv < RS_THREADS / 64; ++wv) wcnt[wv][t] = 0;
     __syncthreads();
     const int p = tile0 + i * RS_THREADS + t;
     const bool ok = p < n;
-    uint64_t key = 0;
-    int32_t val = 0;
-    int d = 0;
-    if (ok) {
-      key = keys_in[p];
-      val = vals_in[p];
-      d = (int)((key >> shift) & 255);
-    }
+    const uint64_t key = kk[i];
+    const int32_t val = vv[i];
+    const int d = ok ? (int)((key >> shift) & 255) : 0;
     // peers: lanes of this wave with the same digit (8 ballots)
     uint64_t peers = __ballot(ok);
 #pragma unroll
