@@ -76,9 +76,9 @@ class WecArgs(C.Structure):
 
 
 class EdgeBwdArgs(C.Structure):
-    _fields_ = [("rows", i32), ("nblk", i32), ("wtpk", vp * 4), ("g", vp), ("g2", vp), ("gidx", vp), ("g3", vp),
-                ("act", vp * 3), ("mask", vp * 3), ("de", vp), ("g0", vp), ("dw_partial", vp), ("db_partial", vp),
-                ("stamps", vp)]
+    _fields_ = [("rows", i32), ("nblk", i32), ("wpk", vp * 4), ("bias", vp * 4), ("ln_g", vp), ("e", vp),
+                ("proj", vp), ("src", vp), ("dst", vp), ("g", vp), ("g2", vp), ("de", vp), ("g0", vp),
+                ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp)]
 
 
 class PackDesc(C.Structure):
@@ -188,7 +188,7 @@ def lib():
             "agn_scatter_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
             "agn_wec_blocks": (i32, [i32]),
             "agn_edge_bwd_blocks": (i32, [i32]),
-            "agn_edge_features": (i32, [i32, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
+            "agn_edge_features": (i32, [i32, C.c_int64, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
             "agn_normalize": (i32, [i32, i32, vp, i32, vp, vp, vp, i32, i32, vp]),
             "agn_col_stats_temp_bytes": (C.c_size_t, [i32, i32]),
             "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),

@@ -276,38 +276,39 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
     return a.ln_rows
 
 
-STAMPS = None  # diagnostics: a uint64 device tensor of 2*4*8*32 entries -> agn_edge_bwd_fused phase clocks
+STAMPS = None  # diagnostics: a uint64 device tensor of 2*8*8*16 entries (a -DAGN_EB_STAMPS library)
 
 
-def fused_edge_bwd_ok(rows, dtype, hidden, nlin, has_ln, acts, hpre):
+def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
     """agn_edge_bwd_fused applies: bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN) large
-    enough for the persistent kernels, saves in the AGN_TILED layout. Opt-in (AEROGNN_FUSED_EDGE_BWD=1):
-    it is exact (tests/test_gpu_fullsize.py) but measured slower than the split path
-    (agn_mlp_backward + agn_wgrad) at C3 — DESIGN.md §9 has the phase clocks."""
+    enough for the persistent kernels. Then the training forward saves nothing for the edge chain
+    and one launch recomputes it in the backward (csrc/edge_bwd.hip). Opt-in with
+    AEROGNN_FUSED_EDGE_BWD=1 while the split path (saved activations, agn_mlp_backward +
+    agn_wgrad) is the faster one on MI355X (fused edge backward)."""
     import os
-    return (os.environ.get("AEROGNN_FUSED_EDGE_BWD", "0") == "1" and dtype == torch.bfloat16 and hidden == 128
-            and nlin == 4 and has_ln and rows >= 64 * 1024 and hpre is not None and is_tiled(hpre)
-            and len(acts) == 3 and all(is_tiled(t) and _mask_of(t) is not None for t in acts))
+    return (os.environ.get("AEROGNN_FUSED_EDGE_BWD", "0") != "0" and dtype == torch.bfloat16 and hidden == 128
+            and nlin == 4 and has_ln and rows >= 64 * 1024)
 
 
-def edge_bwd_fused(*, rows, wtpk, g, g2, gidx, g3, acts, de, g0, tag=None, cost=None):
-    """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32) after the
-    fixed-order slab reduction (agn_wgrad_reduce)."""
+def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None):
+    """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm
+    partials [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce)."""
     lib = L.lib()
-    dev = g3.device
+    dev = e.device
     H = 128
     nblk = int(lib.agn_edge_bwd_blocks(int(rows)))
     dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
     dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
+    lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
     a = L.EdgeBwdArgs()
     a.rows, a.nblk = int(rows), nblk
     for i in range(4):
-        a.wtpk[i] = wtpk[i]
-    a.g, a.g2, a.gidx, a.g3 = ptr(g), ptr(g2), ptr(gidx), ptr(g3)
-    for i in range(3):
-        a.act[i] = ptr(acts[i])
-        a.mask[i] = ptr(_mask_of(acts[i]))
-    a.de, a.g0, a.dw_partial, a.db_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp)
+        a.wpk[i] = wpk[i]
+        a.bias[i] = bias[i]
+    a.ln_g = ln_g
+    a.e, a.proj, a.src, a.dst = ptr(e), ptr(proj), ptr(src), ptr(dst)
+    a.g, a.g2 = ptr(g), ptr(g2)
+    a.de, a.g0, a.dw_partial, a.db_partial, a.ln_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp), ptr(lnp)
     a.stamps = ptr(STAMPS)
     with timed(tag, cost):
         check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
@@ -319,7 +320,7 @@ def edge_bwd_fused(*, rows, wtpk, g, g2, gidx, g3, acts, de, g0, tag=None, cost=
         b.d[l] = L.WgradDesc(None, None, H, H, H, H, int(rows), H, ptr(dwp[l * nblk * H * H:]), ptr(dbp[l * nblk * H:]),
                              ptr(dw[l]), ptr(db[l]), 0, 0, nblk, 0)
     check(lib.agn_wgrad_reduce(C.byref(b), nblk, stream()), "wgrad_reduce")
-    return dw, db
+    return dw, db, lnp, nblk
 
 
 def reduce_partials(partial, nw, n, out):
@@ -402,7 +403,7 @@ class WGrad:
             for j, (G, X, dw, db) in enumerate(live):
                 b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], logical_rows(G),
                                      dw.stride(0), None, None, ptr(dw), ptr(db), int(is_tiled(G)), int(is_tiled(X)), 0, 0)
-            check(lib.agn_wgrad_plan(C.byref(b)), "wgrad_plan")  # splits in proportion to rows
+            check(lib.agn_wgrad_plan(C.byref(b)), "wgrad_plan")  # one uniform split count, from the largest desc
             sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], b.d[j].nsplit))
                      for j, (G, X, _, _) in enumerate(live)]
             bsz = [b.d[j].nsplit * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0
@@ -498,3 +499,11 @@ def cost_wec_bwd(E, N, out, s, hid=64):
 def cost_node_bwd(N, H, s, nlin):
     per = H * s + H * s + (nlin - 1) * mask_bytes(H) + 8 + nlin * H * s + 2 * H * s  # g, hpre, masks, ...
     return N * per, 2 * N * H * (H * (nlin - 1) + 2 * H)
+
+
+def cost_edge_bwd_fused(E, N, H, s):
+    """agn_edge_bwd_fused: per edge the ids, e, the sender's projection row, g, and de + G0 written
+    (+ the row re-reads of g for de, L2); per receiver its P_d row and dAgg row."""
+    per = 8 + H * s * 3 + H * s * 2
+    flops = 2 * E * H * H * (4 + 2 + 4 + 3)  # forward 4 + recompute 2 + dX 4 + dW 3 Linears
+    return E * per + N * 2 * H * s, flops

@@ -37,7 +37,10 @@ def compute_edge_attr(data=None, *, pos=None, edge_index=None, perm=None, stats=
     edge_index = data.edge_index if edge_index is None else edge_index
     require_device(pos, edge_index, perm)
     p32 = _f32(pos)
-    ei = edge_index.contiguous()
+    # the kernel reads int64 indices: other integer dtypes are converted (int32 levels included)
+    ei = edge_index.long().contiguous()
+    if perm is not None:
+        perm = perm.long().contiguous()
     ne = ei.shape[1] if perm is None else perm.numel()
     out = torch.empty(ne, p32.shape[1] + 1, dtype=torch.float32, device=p32.device)
     mean = std = None
@@ -46,9 +49,8 @@ def compute_edge_attr(data=None, *, pos=None, edge_index=None, perm=None, stats=
         require_device(mean, std)
         if mean.numel() != p32.shape[1] + 1 or std.numel() != p32.shape[1] + 1:
             raise ValueError("edge normalization stats must have pos_dim + 1 entries")
-    check(L.lib().agn_edge_features(int(ne), int(p32.shape[1]), ptr(ei), ptr(p32), p32.stride(0),
-                                    ptr(perm.contiguous() if perm is not None else None), ptr(mean), ptr(std),
-                                    ptr(out), stream()), "edge_features")
+    check(L.lib().agn_edge_features(int(ne), int(ei.shape[1]), int(p32.shape[1]), ptr(ei), ptr(p32), p32.stride(0),
+                                    ptr(perm), ptr(mean), ptr(std), ptr(out), stream()), "edge_features")
     return out if dtype is None else out.to(dtype)
 
 
@@ -131,7 +133,7 @@ def collate(data_list, keys=("x", "edge_attr", "y", "pos")):
     ne = [int(d.edge_index.shape[1]) for d in data_list]
     node_off = torch.tensor([0] + nn, dtype=torch.int64).cumsum(0).to(dev)
     edge_off = torch.tensor([0] + ne, dtype=torch.int64).cumsum(0).to(dev)
-    ei = torch.cat([d.edge_index for d in data_list], 1).contiguous()
+    ei = torch.cat([d.edge_index.long() for d in data_list], 1).contiguous()  # agn_collate: int64, in place
     require_device(ei)
     batch = torch.empty(sum(nn), dtype=torch.int64, device=dev)
     check(L.lib().agn_collate(len(data_list), int(sum(ne)), int(sum(nn)), ptr(edge_off), ptr(node_off), ptr(ei),

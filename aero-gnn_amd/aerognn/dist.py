@@ -121,14 +121,18 @@ class GradAllReduce:
         self._armed = True
         self._works = {}
         self._pending = [len(b) for b in self.buckets]
+        self._next = 0
 
     def _hook(self, bi):
         def fire(_p):
             if not self._armed:
                 return
             self._pending[bi] -= 1
-            if self._pending[bi] == 0:
-                self._launch(bi)
+            # RCCL matches collectives across ranks by call order: launch buckets strictly in
+            # index order (as DDP's reducer does), each as soon as it and all before it are ready
+            while self._next < len(self.buckets) and self._pending[self._next] == 0:
+                self._launch(self._next)
+                self._next += 1
         return fire
 
     def _launch(self, bi):
@@ -148,7 +152,7 @@ class GradAllReduce:
         rank, ws = world()
         if ws <= 1:
             return
-        for bi in range(len(self.buckets)):
+        for bi in range(len(self.buckets)):  # the rest, in index order
             if bi not in self._works:
                 self._launch(bi)
         self._armed = False

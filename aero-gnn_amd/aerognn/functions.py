@@ -21,7 +21,8 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_bwd_ok, bwd_nblocks,
+from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
+                   cost_edge_bwd_fused,
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
@@ -348,7 +349,9 @@ class GMPFn(torch.autograd.Function):
         es, ns = spec.edge, spec.node
         e_out = torch.empty_like(e)
         x_out = torch.empty_like(x)
-        ea, ehp, est = _alloc_saves(es, E, dt, dev, train)
+        # fused edge backward: the chain is recomputed there, the forward saves nothing for it
+        fused = train and spec.trick and fused_edge_train_ok(E, dt, H, es.nlin, es.ln is not None)
+        ea, ehp, est = _alloc_saves(es, E, dt, dev, train and not fused)
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         P = None
         if spec.trick:
@@ -366,7 +369,8 @@ class GMPFn(torch.autograd.Function):
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
                         resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
-                        tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin, train)))
+                        tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
+                                                                                            train and not fused)))
         else:
             se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
             ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
@@ -388,6 +392,7 @@ class GMPFn(torch.autograd.Function):
                                                    cost_node_fwd(E, N, H, x.element_size(), ns.nlin, train)))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
+        ctx.fused, ctx.proj = fused, (P if fused else None)
         ctx.save_for_backward(x, e)
         # an unused e' (the U-Net restores fine edges from the skip, bsms_mgn.py:203) arrives as
         # None instead of a materialised [E,H] zero tensor; the kernels read it as zero
@@ -418,24 +423,19 @@ class GMPFn(torch.autograd.Function):
         if spec.aggregation == "mean":  # scatter_mean backward: / max(deg, 1)
             dagg = gather_rows(N, H, None, dagg, torch.empty_like(dagg), cnt_ptr=lv.rowptr)
         # ---- EdgeBlock: d(e) (+ residual), pre-activation grads
-        fused = spec.trick and es.ln is not None and fused_edge_bwd_ok(E, dt, H, es.nlin, True, ea or [], ehp)
-        nb_e = bwd_nblocks(E)
-        part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
+        fused = ctx.fused
         de = torch.empty_like(e)
         sz = x.element_size()
         if fused:
-            # LayerNorm backward alone (G3, LN parameter partials), then the fused chain + dW kernel
-            g3 = tiled_empty(E, H, dt, dev)
-            nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=1, out_dim=H, in_dim=H, wtpk=[es.wtpk()[-1]],
-                                acts=[], g=ge, g2=dagg, gidx=lv.dst, gpre=[g3], ln_g=es.lnp()[0], hpre=ehp,
-                                stats=est, din=[], ln_partial=part_e, tag="edge_ln_bwd",
-                                cost=with_alg(0, (E * (3 * H * sz + 12) + N * H * sz, 0)))
+            # one launch: forward recompute, LayerNorm backward, chain rule, dW1..dW3 / db1..db3
             g0 = torch.empty(E, H, dtype=dt, device=dev)
-            dW13, db13 = edge_bwd_fused(rows=E, wtpk=es.wtpk(), g=ge, g2=dagg, gidx=lv.dst, g3=g3, acts=ea, de=de,
-                                        g0=g0, tag="edge_bwd",
-                                        cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True),
-                                                      (E * (H * sz * 7 + 24 + 4) + N * H * sz, 2 * E * H * H * 7)))
+            dW13, db13, part_e, nb_e = edge_bwd_fused(
+                rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=ctx.proj, src=lv.src, dst=lv.dst,
+                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd",
+                cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True), cost_edge_bwd_fused(E, N, H, sz)))
         else:
+            nb_e = bwd_nblocks(E)
+            part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
             gpre_e = _alloc_gpre(es, E, dt, dev, rowmajor=(0,) if spec.trick else ())
             if spec.trick:
                 din = [(H, de, True)]

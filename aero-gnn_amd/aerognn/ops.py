@@ -128,15 +128,20 @@ def _(src, index, rowptr=None):
 
 def _gather_ctx(ctx, inputs, output):
     src, index, rowptr = inputs
-    ctx.save_for_backward(index)
+    ctx.save_for_backward(index, rowptr)
     ctx.n = src.shape[0]
-    ctx.mean = rowptr is not None
 
 
 def _gather_bwd(ctx, g):
-    (index,) = ctx.saved_tensors
-    # d src[r] = sum over i with index[i] == r of g[i] (/ group size when the forward divided)
-    return torch.ops.aerognn.scatter_sum(g, index, ctx.n, ctx.mean), None, None
+    index, rowptr = ctx.saved_tensors
+    # d src[r] = sum over i with index[i] == r of g[i], divided by the caller's group size
+    # max(rowptr[r+1] - rowptr[r], 1) when the forward divided by it (any rowptr, not only
+    # group_ptr(index))
+    d = torch.ops.aerognn.scatter_sum(g, index, ctx.n, False)
+    if rowptr is not None:
+        cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).to(d.dtype)
+        d = d / cnt[:, None]
+    return d, None, None
 
 
 torch.library.register_autograd("aerognn::gather_rows", _gather_bwd, setup_context=_gather_ctx)

@@ -600,6 +600,24 @@ AGN_DEV void gemm(f32x16 (&acc)[NT], const BOp<T, NR>& b, int nu, const uint4* l
   }
 }
 
+// ---------------------------------------------------------------- LayerNorm element steps
+// Written with explicit fused operations: under -ffp-contract=fast the compiler's SLP
+// vectorisation otherwise contracts some elements of a row (fma) and not others (packed mul +
+// add), per kernel, so two kernels evaluating the same LayerNorm would round differently. Every
+// kernel that computes or differentiates the chain's LayerNorm uses these.
+AGN_DEV float ln_sq_acc(float q, float d) { return __builtin_fmaf(d, d, q); }  // q + d^2
+// backward pass 1: c1 += g*gamma, c2 += (g*gamma) * xhat
+AGN_DEV void ln_bwd_acc(float& c1, float& c2, float g, float gm, float xh) {
+  const float gg = g * gm;
+  c1 = c1 + gg;
+  c2 = __builtin_fmaf(gg, xh, c2);
+}
+// backward pass 2: (g*gamma - c1 - xhat*c2) * rstd
+AGN_DEV float ln_bwd_out(float g, float gm, float c1, float c2, float xh, float rstd) {
+  const float t = __builtin_fmaf(g, gm, -c1);
+  return __builtin_fmaf(-xh, c2, t) * rstd;
+}
+
 // ---------------------------------------------------------------- wave reductions
 AGN_DEV float xor32(float v) { return __shfl_xor(v, 32, 64); }
 

@@ -13,13 +13,14 @@ namespace {
 // then optionally (v - mean) / std per column (dataset.py:403). The norm accumulates the squares
 // with fused multiply-adds in component order, sqrt in fp32 (torch's CPU reduction order; it can
 // differ from torch CPU by one ulp where its vectorised path regroups).
-__global__ void edge_features_kernel(int ne, int pdim, const int64_t* __restrict__ ei, const float* __restrict__ pos,
+__global__ void edge_features_kernel(int ne, int64_t e_total, int pdim, const int64_t* __restrict__ ei,
+                                     const float* __restrict__ pos,
                                      int pos_ld, const int64_t* __restrict__ perm, const float* __restrict__ mean,
                                      const float* __restrict__ std, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= ne) return;
   const int64_t e = perm ? perm[i] : i;
-  const int64_t s = ei[e], d = ei[(int64_t)ne + e];
+  const int64_t s = ei[e], d = ei[e_total + e];  // row 1 of the [2][e_total] edge_index
   float v[4] = {0.f, 0.f, 0.f, 0.f};
   float acc = 0.f;
   for (int c = 0; c < pdim; ++c) {
@@ -75,8 +76,9 @@ __global__ void colfinish_kernel(int n, int k, int nb, const double* __restrict_
     mean64[c] = s / (double)n;
     mean[c] = (float)(s / (double)n);
   } else {
-    const float sd = (float)sqrt(s / (double)(n > 1 ? n - 1 : 1));
-    std[c] = sd > eps ? sd : eps;
+    // torch.std_mean (unbiased: n = 1 gives NaN) then clamp(min=eps), which keeps a NaN
+    const float sd = (float)sqrt(s / (double)(n - 1));
+    std[c] = sd != sd ? sd : fmaxf(sd, eps);
   }
 }
 
@@ -113,12 +115,13 @@ inline int status() {
 
 extern "C" {
 
-int agn_edge_features(int ne, int pdim, const int64_t* edge_index, const float* pos, int pos_ld, const int64_t* perm,
-                      const float* mean, const float* std, float* out, void* stream) {
-  if (ne < 0 || pdim < 1 || pdim > 3 || (!mean) != (!std)) return AGN_E_ARG;
+int agn_edge_features(int ne, int64_t e_total, int pdim, const int64_t* edge_index, const float* pos, int pos_ld,
+                      const int64_t* perm, const float* mean, const float* std, float* out, void* stream) {
+  if (ne < 0 || e_total < 0 || pdim < 1 || pdim > 3 || (!mean) != (!std)) return AGN_E_ARG;
+  if (!perm && ne > e_total) return AGN_E_SHAPE;
   if (ne == 0) return 0;
-  hipLaunchKernelGGL(edge_features_kernel, dim3((ne + 255) / 256), dim3(256), 0, (hipStream_t)stream, ne, pdim,
-                     edge_index, pos, pos_ld, perm, mean, std, out);
+  hipLaunchKernelGGL(edge_features_kernel, dim3((ne + 255) / 256), dim3(256), 0, (hipStream_t)stream, ne, e_total,
+                     pdim, edge_index, pos, pos_ld, perm, mean, std, out);
   return status();
 }
 

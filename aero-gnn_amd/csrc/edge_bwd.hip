@@ -1,373 +1,641 @@
-// Fused backward of the sum-trick edge MLP with in-kernel weight gradients (gfx950, bf16, H=128).
+// Fused training backward of the sum-trick edge MLP (gfx950, bf16, H = 128): forward recompute,
+// chain rule and in-kernel weight gradients in ONE persistent launch.
 //
-// Reference chain (mgnLayer.py:72-105, residual :205):
+// Reference chain (models/mgnLayer.py:72-105, residual :205):
 //   h0 = e W_e^T + P_s[src] + P_d[dst];  a1 = relu(h0); h1 = a1 W1^T + b1; a2 = relu(h1);
 //   h2 = a2 W2^T + b2; a3 = relu(h2); h3 = a3 W3^T + b3; e' = e + LN(h3).
-// Backward for one edge tile (S = dL/de' = g + g2[dst]):
-//   G3 = LN'(S)  -> dW3 += G3^T a3, db3 += sum G3
-//   G2 = (G3 W3) . [a3 > 0] -> dW2 += G2^T a2 ...  G1 -> dW1 += G1^T a1;  G0 = (G1 W1) . [a1 > 0]
-//   de = G0 W_e + S;  G0 is written (its sender / receiver sums are dP_s / dP_d; dW_e = G0^T e).
+// Backward of one 32-edge tile (S = dL/de' = g + dAgg[dst]):
+//   G3 = LN'(S);  dW3 += G3^T a3, db3 += sum G3;  G2 = (G3 W3) . [a3 > 0];  ... ;
+//   G0 = (G1 W1) . [a1 > 0];  de = G0 W_e + S.
+//   G0 is written (its sender / receiver segment sums are dP_s / dP_d, dW_e = G0^T e goes to
+//   agn_wgrad); G1..G3, a1..a3 and h3 never reach HBM, and the training forward saves nothing.
 //
-// The split path (agn_mlp_backward + agn_wgrad) writes G0..G3 (1 KB/edge) and agn_wgrad reads them
-// back together with the saved activations (2 KB/edge). Here one persistent launch keeps dW1..dW3
-// in registers for its whole lifetime, so G1..G3 never reach HBM:
-//
-//  * one 256-thread block per CU (4 waves, one per SIMD: 512 registers each); the block walks
-//    ROUNDS of 128 edges (four 32-row tiles, tile p on wave p) in CSC order, XCD-grouped like
-//    the resident kernels;
-//  * per layer step L = 3, 2, 1 the round's G_L and X_L (= a_L) sit in LDS as [128 rows][128]
-//    bf16 images (XOR-swizzled 8-byte units, see swz): the dW MFMAs read 8-row columns of both
-//    with ds_read_b64_tr_b16 (k = rows), the chain MFMA (rows on lanes, common.hpp) reads its B
-//    operand rows straight from the G image and W_L^T from a double-buffered LDS copy that the
-//    previous step prefetched with global_load_lds;
-//  * wave w owns dW_L[0..127][32w..32w+31] for L = 1..3: 4 accumulator tiles per L, 192
-//    registers for the whole launch; its 32 dW MFMAs per step match its 32 chain MFMAs;
-//  * the LayerNorm backward runs before this kernel (an LN-only agn_mlp_backward writes G3);
-//    db_L are column sums of the G_L images.
-// Measured: exact, but latency-bound at one wave per SIMD, so it is opt-in.
-// Partials per block go to slabs summed in fixed order by agn_wgrad_reduce / agn_colsum: no atomics.
+// Work split (one 512-thread workgroup per CU, two waves per SIMD):
+//  * waves 0-3 ("chain waves", one per SIMD) each own a 32-edge tile per round: they recompute
+//    h0..h3 from e and the gathered projection rows (bitwise the forward kernel's values: same
+//    operands, same MFMA order), run the LayerNorm backward and the chain rule, and hand each
+//    layer's (G_L, a_L) to the dW waves in 16-row items through an LDS ring;
+//  * waves 4-7 ("dW waves", one per SIMD) own a 64x64 quarter of dW1..dW3 each (192 accumulator
+//    registers for the whole launch) and consume every item in a fixed order (round, layer,
+//    half, chain wave): the fp32 sums are deterministic;
+//  * all four Linears live in LDS as ONE image each, read both ways: rows (ds_read_b128, the
+//    forward's A = W fragments) and columns (ds_read_b64_tr_b16, the backward's A = W^T
+//    fragments). The image is layout (a) of cdna_hip_programming.md T10 over the packed forward
+//    operand (agn_pack, trans = 0), whose k order is the acc-register order of common.hpp; the
+//    transposed reads pick their 8-byte pieces so that each lane gets the same 8 values, in the
+//    same order, as the split path's packed W^T fragments (agn_pack, trans = 1).
+// The ring holds 3 slots of 8 KB (G_L and a_L for 16 rows, layout (a) images read with
+// ds_read_b64_tr_b16 by the dW MFMAs, k = rows). A chain wave writes item n into slot n % 3 once
+// item n - 3 has been consumed by all four dW waves; LDS counters (filled / consumed) order the
+// hand-offs, no workgroup barrier runs inside the main loops.
+// Per-workgroup partials (dW, db, LayerNorm) go to slabs that agn_wgrad_reduce / agn_colsum sum in
+// fixed order: no atomics on HBM.
 #include "common.hpp"
 #include "aerognn.h"
-
-#include <type_traits>
 
 using namespace agn;
 
 namespace {
 
 constexpr int H = 128;
-constexpr int EB_WAVES = 4;                 // one wave per SIMD: 512 registers each
-constexpr int EB_THREADS = 64 * EB_WAVES;
-constexpr int EB_ROUND = 32 * EB_WAVES;     // rows per round: one 32-row tile per wave
-constexpr int LDI = 128;                    // LDS image row stride (bf16), unpadded: bank spread by swizzle
-constexpr int WUNITS = 4 * 8 * 64;          // packed 128x128 operand: [ot 4][ku 8][lane 64] x 16 B = 32 KB
+constexpr int NT = 4;                  // 32-feature tiles per row
+constexpr int NR = 64;                 // acc registers per row half
+constexpr int CW = 4;                  // chain waves
+constexpr int NWAVE = 8;               // chain + dW waves
+constexpr int NTHR = 64 * NWAVE;
+constexpr int NSLOT = 3;
+constexpr int IMG_B = H * H * 2;       // one 128 x 128 bf16 image (32 KB)
+constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
+constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
+constexpr int OFF_RING = 4 * IMG_B;
+constexpr int OFF_PV = OFF_RING + NSLOT * SLOT_B;  // fp32 [4][H]: b1, b2, b3, LN gamma
+constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[4], consumed[4]
+constexpr int OFF_LNP = OFF_FLAG + 32;             // fp32 [CW][2][H]: LayerNorm partials per chain wave
+constexpr int LDS_B = OFF_LNP + CW * 2 * H * 4;
+static_assert(LDS_B <= 160 * 1024, "LDS budget");
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// LDS images [rows][128] bf16 are stored with an XOR swizzle of their 8-byte units:
-// unit u of row r sits at u ^ f(r & 31), f(x) = (x & 3) << 3 | x >> 2. Both read patterns are then
-// conflict-free: a row per lane (32 rows, one unit: f injective over 0..31) and the transposed
-// reads (rows kb..kb+3 x 8 units per 32-lane half: q << 3 picks 4 distinct 8-unit blocks).
-AGN_DEV int swz(int r, int col) {  // element offset of (row, col), col a multiple of 4
-  const int x = r & 31;
-  return r * LDI + (col ^ ((((x & 3) << 3) | (x >> 2)) << 2));
+// Layout (a) of a [rows][128] bf16 image: 8-row x 32-column subtiles of 512 B, 16-B chunk ch of
+// row r at the byte offset below. Row reads of a 32x32x16 operand (one 16-B chunk per lane, 32
+// rows) and transposed reads (4 rows x 32 columns per 32-lane half) are both conflict-free, and
+// the offsets split into a per-lane part plus immediates (4096 per 16 rows, 512 per 32 columns).
+AGN_DEV int aoff(int r, int ch) {
+  return 2048 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
 }
 
-// 8 consecutive rows (kb..kb+7) of one column of an LDS image: the MFMA A/B fragment with k = rows
-AGN_DEV bf16x8 tr8(const bf16* img, int kb, int col_base, int lane) {
-  const int q = (lane & 15) >> 2, pp = lane & 3;
-  const bf16* a0 = img + swz(kb + q, col_base + 4 * pp);
-  const bf16* a1 = img + swz(kb + 4 + q, col_base + 4 * pp);
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a1));
-  const bf16x4 l4 = __builtin_bit_cast(bf16x4, lo);
-  const bf16x4 h4 = __builtin_bit_cast(bf16x4, hi);
-  return bf16x8{l4[0], l4[1], l4[2], l4[3], h4[0], h4[1], h4[2], h4[3]};
+// feature held at image position p (the acc-register order of common.hpp swaps bits 2 and 3
+// within each 16-feature block); an involution
+AGN_DEV int phi(int p) { return (p & ~12) | ((p & 4) << 1) | ((p & 8) >> 1); }
+
+AGN_DEV bf16x8 tr_pair(const char* lo, const char* hi) {
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lo));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(hi));
+  const bf16x4 x = __builtin_bit_cast(bf16x4, a), y = __builtin_bit_cast(bf16x4, b);
+  return bf16x8{x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
 }
 
-// B operand of the rows-on-lanes chain MFMA for k-step u (features 16u+4h..+3 | 16u+8+4h..+3 of
-// the lane's row, common.hpp acc-register order) from a row of an LDS image
-AGN_DEV bf16x8 brow(const bf16* img, int r, int u, int h) {
-  const u32x2 lo = *reinterpret_cast<const u32x2*>(img + swz(r, 16 * u + 4 * h));
-  const u32x2 hi = *reinterpret_cast<const u32x2*>(img + swz(r, 16 * u + 8 + 4 * h));
-  return __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
-}
-// 8-byte unit store / load of an LDS image
-AGN_DEV void put4(bf16* img, int r, int col, uint32_t a, uint32_t b) {
-  *reinterpret_cast<u32x2*>(img + swz(r, col)) = u32x2{a, b};
-}
-AGN_DEV u32x2 get4(const bf16* img, int r, int col) { return *reinterpret_cast<const u32x2*>(img + swz(r, col)); }
-
-// dW accumulation with the accumulator pinned to AGPRs ("+a"): the dW tiles live for the whole
-// launch (192 AGPRs per lane), so the VALU working set keeps all 256 arch VGPRs.
-AGN_DEV void mfma_acc(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+AGN_DEV void mfma(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
 }
 
-// Wait for every outstanding vector-memory operation of this wave, global_load_lds included
-// (the LDS copy is only visible to the other waves after this wait and the next barrier).
-AGN_DEV void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Async copy of one packed 32 KB operand into an LDS buffer: 8 x 1 KB per wave (lane-linear).
-AGN_DEV void glds_weights(uint4* dst, const void* src, int wave, int lane) {
-  const char* g = reinterpret_cast<const char*>(src);
+// acc[ot] += W[ot rows] . X^T for the 8 k-steps of an H-wide operand (A = W row fragments of an
+// LDS image): the order of common.hpp gemm(), so the sums are bitwise the forward kernel's
+AGN_DEV void gemm_rows(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const char* img, int lane) {
+  const int i = lane & 31, hh = lane >> 5;
+  const int base = 2048 * (i >> 3) + 64 * (i & 7);
+  const int x = (i >> 2) & 3;
+  const char* pe = img + base + 16 * (hh ^ x);        // k-steps u even: chunk 2u + hh, (ch & 3) = hh
+  const char* po = img + base + 16 * ((2 + hh) ^ x);  // u odd: (ch & 3) = 2 + hh
+  // fragments stream two (u, ot) steps ahead (8 registers in flight)
+  auto frag = [&](int idx) {
+    const int u = idx >> 2, ot = idx & 3;
+    return *reinterpret_cast<const uint4*>((u & 1 ? po : pe) + 512 * (u >> 1) + 8192 * ot);
+  };
+  uint4 f0 = frag(0), f1 = frag(1);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int piece = wave * 8 + j;  // 32 pieces of 1 KB
-    __builtin_amdgcn_global_load_lds(g + piece * 1024 + lane * 16,
-                                     (__attribute__((address_space(3))) void*)(dst + piece * 64), 16, 0, 0);
+  for (int idx = 0; idx < 8 * NT; ++idx) {
+    const uint4 cur = f0;
+    f0 = f1;
+    if (idx + 2 < 8 * NT) f1 = frag(idx + 2);
+    b.mfma(acc[idx & 3], cur, idx >> 2);
+    __builtin_amdgcn_sched_barrier(0);  // keep the 2-deep prefetch: no hoisting of all 32 reads
   }
 }
 
-// One 32-row tile of an AGN_TILED [rows][128] bf16 matrix (8 KB: 8 units per lane, 1 KB per
-// instruction), moved to rows 32p.. of an LDS image in natural feature order.
-struct TiledTile {
-  uint4 v[8];
-  AGN_DEV void load(const void* base, int tile, int ntiles, int rows, int lane) {
-    const uint4* b = reinterpret_cast<const uint4*>(base) + (size_t)tile * 8 * 64;
-    const bool ok = tile < ntiles && tile * 32 + (lane & 31) < rows;  // padded rows are never written
+// acc[ot] = W^T[ot rows] . G^T (accumulators start at zero): A = W^T fragments by transposed reads of the same image. Lane
+// (i, hh) of k-step u needs W[16u + 8(j>>2) + 4hh + (j&3)][32ot + i], j = 0..7 (agn_pack trans = 1):
+// rows 16u + 4hh + q (q = 0..3) and 16u + 8 + 4hh + q; lane 4q + p of its 16-lane group g supplies
+// the 8-byte piece (chunk 4ot + 2(g&1) + (p&1), half p>>1), so the column lane t of the group
+// receives is position 32ot + 16(g&1) + phi(t), i.e. feature 32ot + i.
+AGN_DEV void gemm_cols(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const char* img, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, hh = lane >> 5;
+  const int xx = 2 * (g & 1) + (p & 1);
+  const char* r1 = img + 64 * (4 * hh + q) + 16 * (xx ^ hh) + 8 * (p >> 1);
+  const char* r2 = img + 2048 + 64 * (4 * hh + q) + 16 * (xx ^ (hh + 2)) + 8 * (p >> 1);
+  auto frag = [&](int idx) {
+    const int u = idx >> 2, ot = idx & 3;
+    return tr_pair(r1 + 4096 * u + 512 * ot, r2 + 4096 * u + 512 * ot);
+  };
+  bf16x8 f0 = frag(0), f1 = frag(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = ok ? b[i * 64 + lane] : uint4{0u, 0u, 0u, 0u};
+  for (int idx = 0; idx < 8 * NT; ++idx) {
+    const bf16x8 cur = f0;
+    f0 = f1;
+    if (idx + 2 < 8 * NT) f1 = frag(idx + 2);
+    if (idx < NT) acc[idx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, b.u[0], f32x16{}, 0, 0, 0);
+    else mfma(acc[idx & 3], cur, b.u[idx >> 2]);
+    __builtin_amdgcn_sched_barrier(0);
   }
-  // unit (i, lane = c + 32 hh) holds features 16i+4hh..+3 | 16i+8+4hh..+3 of row c
-  AGN_DEV void store(bf16* img, int p, int lane) const {
-    const int r = 32 * p + (lane & 31), h = lane >> 5;
+}
+
+// acc = bias (fp32 [H] in LDS), acc layout
+AGN_DEV void acc_bias(f32x16 (&acc)[NT], const float* pv, int h) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const u32x4 x = __builtin_bit_cast(u32x4, v[i]);
-      put4(img, r, 16 * i + 4 * h, x[0], x[1]);
-      put4(img, r, 16 * i + 8 + 4 * h, x[2], x[3]);
+  for (int q = 0; q < 4 * NT; ++q) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(pv + 8 * q + 4 * h);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+  }
+}
+
+// Spin on an LDS counter. Bounded (about a second): a protocol error then yields wrong sums instead
+// of a wave that never finishes.
+AGN_DEV void wait_ge(int* p, int v) {
+  for (int spin = 0; spin < (1 << 24); ++spin) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  asm volatile("" ::: "memory");
+}
+// scheduling fence: keeps the machine scheduler from hoisting the next phase's LDS reads (bias,
+// gamma) above the current phase's register work, where they would all be live at once
+AGN_DEV void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+AGN_DEV void lgkm_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// the lane id behind a compiler barrier: per-lane LDS offsets derived from it are recomputed in
+// each phase instead of being hoisted out of the tile loop (where they would sit in registers
+// across the whole chain and spill)
+template <typename V> AGN_DEV void opaque(V& v) { asm volatile("" : "+v"(v)); }
+// pin a packed operand in place: IR passes must not sink its computation (and every input it
+// reads) down to the first use, which would keep those inputs live across the work in between
+AGN_DEV void pin(BOp<bf16, NR>& b) {
+#pragma unroll
+  for (int i = 0; i < NR / 8; ++i) opaque(b.u[i]);
+}
+AGN_DEV int fresh_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+
+struct Rounds {  // XCD-grouped round walk (blocks b and b + 8 share an XCD and its L2)
+  int first, end, step;
+  AGN_DEV Rounds(int nrounds) {
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+      const int grp = blockIdx.x & 7, per = (nrounds + 7) / 8;
+      first = grp * per + (blockIdx.x >> 3);
+      end = min(nrounds, (grp + 1) * per);
+      step = gridDim.x >> 3;
+    } else {
+      first = blockIdx.x;
+      end = nrounds;
+      step = gridDim.x;
     }
   }
 };
 
-// A row-major [rows][128] bf16 tile row pair (16 B per lane at features 16i + 8h): the incoming
-// gradient rows of the residual (common.hpp load8_w without the exchange, done at use)
-struct RowTile {
-  uint4 v[8];
-  AGN_DEV void load(const bf16* rowp, int lane) {
+// ------------------------------------------------------------------------------ chain wave
+// Item n = (round, s = 2 (3 - L) + half, chain wave): G_L and a_L of rows 16 half .. 16 half + 15
+// of the wave's tile, as two layout (a) images: unit i of lane (c, hh) = positions 16i + 8hh..+7
+// (chunk 2i + hh) of row c & 15.
+AGN_DEV void produce(char* lds, int n, const BOp<bf16, NR>& G, const BOp<bf16, NR>& X, int half, int lane) {
+  int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
+  int* consumed = filled + 4;
+  const int k = n % NSLOT, j = n / NSLOT;
+  wait_ge(&consumed[k], 4 * j);
+  const int c = lane & 31, hh = lane >> 5;
+  if ((c >> 4) == half) {
+    char* sb = lds + OFF_RING + k * SLOT_B;
+    const int r = c & 15, x = (r >> 2) & 3;
+    const int base = 2048 * (r >> 3) + 64 * (r & 7);
+    const int oe = base + 16 * (hh ^ x), oo = base + 16 * ((2 + hh) ^ x);  // aoff(r, 2i + hh), i even / odd
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const uint4*>(rowp + 16 * i + 8 * (lane >> 5));
+    for (int i = 0; i < 8; ++i) {
+      const int o = (i & 1 ? oo : oe) + 512 * (i >> 1);
+      *reinterpret_cast<uint4*>(sb + o) = __builtin_bit_cast(uint4, G.u[i]);
+      *reinterpret_cast<uint4*>(sb + HALF_B + o) = __builtin_bit_cast(uint4, X.u[i]);
+    }
   }
-  AGN_DEV void zero() {
+  lgkm_drain();
+  if (lane == 0) __hip_atomic_store(&filled[k], j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// G_{L-1} = dA . [a_L > 0] (the split path's AGN_RELU_MASK select, from the packed activation)
+AGN_DEV void relu_select(float (&A)[NR], const f32x16 (&acc)[NT], const BOp<bf16, NR>& act) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = uint4{0u, 0u, 0u, 0u};
-  }
-};
+  for (int i = 0; i < NR; ++i) A[i] = bop_pos<NR>(act, i) ? acc[i / 16][i % 16] : 0.f;
+}
 
-__global__ __launch_bounds__(EB_THREADS, 1) void edge_bwd_fused_kernel(const agn_edge_bwd_args a) {
-  __shared__ uint4 wbuf[2][WUNITS];
-  __shared__ __attribute__((aligned(16))) bf16 gs[EB_ROUND * LDI];
-  __shared__ __attribute__((aligned(16))) bf16 xs[EB_ROUND * LDI];
+// Diagnostic phase clocks (built with -DAGN_EB_STAMPS into a separate library; the product build
+// has none): chain wave w of blocks 0 and 128 stamps s_memtime at 16 points of its first 8 tiles
+// into a.stamps[((sel * 8 + w) * 8 + tile) * 16 + point]; dW wave d stores its total wait and
+// total cycles at point 0 / 1 of slot (sel * 8 + 4 + d) * 8 * 16.
+#ifdef AGN_EB_STAMPS
+#define EB_STAMP(k)                                                                                     \
+  do {                                                                                                  \
+    if (stp && ntile_done < 8 && (lane0 & 63) == 0) stp[ntile_done * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define EB_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
 
-  const int lane0 = threadIdx.x & 63, w = threadIdx.x >> 6;
+AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0) {
+#ifdef AGN_EB_STAMPS
+  unsigned long long* stp = nullptr;
+  if (a.stamps && (blockIdx.x == 0 || blockIdx.x == 128)) stp = a.stamps + ((blockIdx.x == 0 ? 0 : 8) + cw) * 8 * 16;
+  int ntile_done = 0;
+#endif
   const int ntiles = (a.rows + 31) / 32;
-  const int nrounds = (ntiles + EB_WAVES - 1) / EB_WAVES;
-  // XCD-grouped round walk (blocks b and b + 8 share an XCD and its L2)
-  int first, end, step;
-  if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
-    const int grp = blockIdx.x & 7, per = (nrounds + 7) / 8;
-    first = grp * per + (blockIdx.x >> 3);
-    end = min(nrounds, (grp + 1) * per);
-    step = gridDim.x >> 3;
-  } else {
-    first = blockIdx.x;
-    end = nrounds;
-    step = gridDim.x;
+  const int nrounds = (ntiles + CW - 1) / CW;
+  const Rounds rw(nrounds);
+  const float* pv = reinterpret_cast<const float*>(lds + OFF_PV);
+  const bf16* P = reinterpret_cast<const bf16*>(a.proj);
+  int rcount = 0;
+  for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
+    const int cmax = min(CW, ntiles - rd * CW);
+    if (cw >= cmax) continue;
+    EB_STAMP(0);
+    const int nbase = rcount * 6 * CW;  // only a workgroup's last round can be partial
+    const int tile = rd * CW + cw;
+    cbarrier();
+    // per-tile lane id: nothing lane-derived (row addresses, LDS offsets) is hoisted out of the
+    // tile loop, where it would stay live across the whole chain
+    const int lane = fresh_lane(lane0);
+    const int c = lane & 31, h = lane >> 5;
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    const int rr = valid ? row : a.rows - 1;
+    const int sid = a.src[rr], did = a.dst[rr];
+    // incoming gradient row g: loaded now, kept raw (32 registers) through the forward recompute
+    uint4 graw[NR / 8];
+    if (a.g) {
+      const bf16* gp = reinterpret_cast<const bf16*>(a.g) + (size_t)rr * H;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) graw[i] = uint4{0u, 0u, 0u, 0u};
+    }
+    // ---- forward recompute (mlp_fwd_res_kernel's operations, in its order)
+    f32x16 acc[NT];
+    BOp<bf16, NR> a1;  // the only activation kept from the forward pass
+    {
+      const bf16* ps = P + (size_t)sid * (2 * H);
+      const bf16* pd = P + (size_t)did * (2 * H) + H;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        float x[8], y[8];
+        load8_w(x, ps, i, h);
+        load8_w(y, pd, i, h);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
+      }
+      BOp<bf16, NR> eop;
+      float v[NR];
+      load_row_w<bf16, NR>(v, reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
+      eop.set(v);
+      EB_STAMP(1);
+      gemm_rows(acc, eop, lds + 0 * IMG_B, fresh_lane(lane));
+    }
+    cbarrier();
+    a1.template set_relu<NT>(acc);
+    pin(a1);
+    sched_fence();
+    acc_bias(acc, pv + 0 * H, h);
+    gemm_rows(acc, a1, lds + 1 * IMG_B, fresh_lane(lane));
+    cbarrier();
+    {  // a2 is not kept (recomputed from a1 in step 2: 32 MFMAs instead of 32 live registers)
+      BOp<bf16, NR> a2;
+      a2.template set_relu<NT>(acc);
+      pin(a2);
+      sched_fence();
+      acc_bias(acc, pv + 1 * H, h);
+      gemm_rows(acc, a2, lds + 2 * IMG_B, fresh_lane(lane));
+    }
+    cbarrier();
+    {  // a3 is not kept either (recomputed in step 3)
+      BOp<bf16, NR> a3;
+      a3.template set_relu<NT>(acc);
+      pin(a3);
+      sched_fence();
+      acc_bias(acc, pv + 2 * H, h);
+      gemm_rows(acc, a3, lds + 3 * IMG_B, fresh_lane(lane));
+    }
+    EB_STAMP(2);
+    // LayerNorm statistics (mlp_fwd_res_kernel's epilogue)
+    float mean, rstd;
+    {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
+      s += xor32(s);
+      mean = s / (float)H;
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        const float d = acc[i / 16][i % 16] - mean;
+        q = ln_sq_acc(q, d);
+      }
+      q += xor32(q);
+      rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
+    }
+    // the pre-LN row as the split path stores it (bf16, acc order)
+    BOp<bf16, NR> hpk;
+    {
+      float v[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = acc[i / 16][i % 16];
+      hpk.set(v);
+      pin(hpk);
+    }
+    cbarrier();
+    // ---- incoming gradient S = g + dAgg[dst] (mlp_bwd_res_kernel's load_grad_w)
+    float A[NR];
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      float o[8];
+      unpack8_w(o, graw[i]);  // load8_w's exchange + conversion
+#pragma unroll
+      for (int e = 0; e < 8; ++e) A[8 * i + e] = o[e];
+    }
+    sched_fence();
+    add_row_w<bf16, NR>(A, reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H, h);
+    if (!valid) {
+#pragma unroll
+      for (int i = 0; i < NR; ++i) A[i] = 0.f;
+    }
+    // ---- LayerNorm backward (mlp_bwd_res_kernel, its expressions; partials in 16-register
+    // chunks: the butterfly's XOR order 16, 8, 4, 2, 1 gives each feature the same sums)
+    {
+      const float* gmv = pv + 3 * H;
+      float c1 = 0.f, c2 = 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        sched_fence();
+        float B[16];
+#pragma unroll
+        for (int i = 2 * kk; i < 2 * kk + 2; ++i) {
+          float hv[8];
+          unpack8(hv, __builtin_bit_cast(uint4, hpk.u[i]));
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const f32x4 gm = *reinterpret_cast<const f32x4*>(gmv + 16 * i + 8 * j + 4 * h);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 8 * i + 4 * j + e;
+              const float xh = (hv[4 * j + e] - mean) * rstd;
+              ln_bwd_acc(c1, c2, A[r], gm[e], xh);
+              B[r - 16 * kk] = A[r] * xh;
+            }
+          }
+        }
+        // lane c holds the 32-row sums of register 16 kk + c/2 (pairs c, c^1 identical)
+        float* lp = reinterpret_cast<float*>(lds + OFF_LNP) + cw * 2 * H + feat_of(16 * kk + (c >> 1), h);
+        butterfly_reduce<16>(B, lane);
+        if ((c & 1) == 0) lp[0] += B[0];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) B[i] = A[16 * kk + i];
+        butterfly_reduce<16>(B, lane);
+        if ((c & 1) == 0) lp[H] += B[0];
+        opaque(c1);  // the running sums are due now: nothing of this chunk stays live for later
+        opaque(c2);
+      }
+      c1 += xor32(c1);
+      c2 += xor32(c2);
+      c1 /= (float)H;
+      c2 /= (float)H;
+      // pass 2 unpacks h3 and recomputes xhat again: opaque copies keep the compiler from holding
+      // pass 1's 64 unpacked / normalised values live in between
+      opaque(mean);
+      opaque(rstd);
+      int goff = 0;
+      opaque(goff);  // gamma and A * gamma re-read / recomputed, not kept from pass 1
+      const float* gmv2 = gmv + goff;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        sched_fence();
+        float hv[8];
+        u32x4 hr = __builtin_bit_cast(u32x4, hpk.u[i]);
+        opaque(hr);  // unpacked again, not kept from pass 1
+        unpack8(hv, __builtin_bit_cast(uint4, hr));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 gm = *reinterpret_cast<const f32x4*>(gmv2 + 16 * i + 8 * j + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * i + 4 * j + e;
+            const float xh = (hv[4 * j + e] - mean) * rstd;
+            A[r] = ln_bwd_out(A[r], gm[e], c1, c2, xh, rstd);
+          }
+        }
+      }
+    }
+    EB_STAMP(3);
+    // ---- chain rule; every layer's (G_L, a_L) goes to the dW waves
+    BOp<bf16, NR> op;
+    cbarrier();
+    op.set(A);  // G3
+    pin(op);
+    BOp<bf16, NR> a2;
+    {
+      // a2 = relu(a1 W1^T + b1), a3 = relu(a2 W2^T + b2) again (the forward's operations)
+      BOp<bf16, NR> a3;
+      sched_fence();
+      acc_bias(acc, pv + 0 * H, h);
+      gemm_rows(acc, a1, lds + 1 * IMG_B, fresh_lane(lane));
+      cbarrier();
+      a2.template set_relu<NT>(acc);
+      pin(a2);
+      sched_fence();
+      acc_bias(acc, pv + 1 * H, h);
+      gemm_rows(acc, a2, lds + 2 * IMG_B, fresh_lane(lane));
+      cbarrier();
+      a3.template set_relu<NT>(acc);
+      pin(a3);
+      sched_fence();
+      EB_STAMP(4);
+      produce(lds, nbase + 0 * cmax + cw, op, a3, 0, fresh_lane(lane));
+      produce(lds, nbase + 1 * cmax + cw, op, a3, 1, fresh_lane(lane));
+      EB_STAMP(5);
+      gemm_cols(acc, op, lds + 3 * IMG_B, fresh_lane(lane));
+      relu_select(A, acc, a3);
+      EB_STAMP(6);
+    }
+    cbarrier();
+    op.set(A);  // G2
+    pin(op);
+    produce(lds, nbase + 2 * cmax + cw, op, a2, 0, fresh_lane(lane));
+    produce(lds, nbase + 3 * cmax + cw, op, a2, 1, fresh_lane(lane));
+    EB_STAMP(7);
+    gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
+    relu_select(A, acc, a2);
+    EB_STAMP(8);
+    cbarrier();
+    op.set(A);  // G1
+    pin(op);
+    produce(lds, nbase + 4 * cmax + cw, op, a1, 0, fresh_lane(lane));
+    produce(lds, nbase + 5 * cmax + cw, op, a1, 1, fresh_lane(lane));
+    EB_STAMP(9);
+    gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
+    relu_select(A, acc, a1);
+    EB_STAMP(10);
+    cbarrier();
+    op.set(A);  // G0
+    pin(op);
+    op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
+    gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
+    // de = G0 W_e + (g + g2): mlp_bwd_res_kernel's add_grad_w order. The rows are re-read (L2):
+    // opaque indices keep the compiler from holding the first reads' values live since the LN
+    {
+      float v[NR];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) v[i] = acc[i / 16][i % 16];
+      int did2 = did, rr2 = rr;
+      opaque(did2);
+      opaque(rr2);
+      const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did2 * H;
+      if (a.g) {
+        const bf16* g1p = reinterpret_cast<const bf16*>(a.g) + (size_t)rr2 * H;
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) {
+          float x[8], y[8];
+          load8_w(x, g1p, i, h);
+          load8_w(y, g2p, i, h);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[8 * i + e] += x[e] + y[e];
+        }
+      } else {
+        add_row_w<bf16, NR>(v, g2p, h);
+      }
+      store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
+    }
+    EB_STAMP(11);
+#ifdef AGN_EB_STAMPS
+    ++ntile_done;
+#endif
   }
+}
 
-  // wave w owns dW_L[0..127][32w..32w+31] (4 output tiles) for L = 1..3, in AGPRs (mfma_acc)
-  f32x16 dw[3][4];
+// ------------------------------------------------------------------------------ dW wave
+AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
+  int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
+  int* consumed = filled + 4;
+  const int ntiles = (a.rows + 31) / 32;
+  const int nrounds = (ntiles + CW - 1) / CW;
+  const Rounds rw(nrounds);
+  const int ob = 2 * (d >> 1), ib = 2 * (d & 1);  // position blocks: o 32ob.., i 32ib.. (two each)
+  // transposed reads of an item image: rows 8hh + q (+4), positions 32 blk + 16(g&1) + 4p..
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, hh = lane >> 5;
+  const int xx = 2 * (g & 1) + (p >> 1);
+  const int t1 = 2048 * hh + 64 * q + 16 * (xx ^ (2 * hh)) + 8 * (p & 1);
+  const int t2 = 2048 * hh + 64 * (4 + q) + 16 * (xx ^ (2 * hh + 1)) + 8 * (p & 1);
+  f32x16 dw[3][2][2];
+  float dbs[3][2];
 #pragma unroll
   for (int l = 0; l < 3; ++l)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) dw[l][t] = f32x16{};
-  float db[3][4];
+    for (int x = 0; x < 2; ++x) {
+      dbs[l][x] = 0.f;
 #pragma unroll
-  for (int l = 0; l < 3; ++l) db[l][0] = db[l][1] = db[l][2] = db[l][3] = 0.f;
-
-  // prologue: W3^T -> buffer 1 (buffers: W3, W1 in 1; W2, W_e in 0); the first round's G3 and a3
-  glds_weights(wbuf[1], a.wtpk[3], w, lane0);
-  if (first < end) {
-    TiledTile t3;
-    t3.load(a.g3, first * EB_WAVES + w, ntiles, a.rows, lane0);
-    t3.store(gs, w, lane0);
-    t3.load(a.act[2], first * EB_WAVES + w, ntiles, a.rows, lane0);
-    t3.store(xs, w, lane0);
-  }
-  vm_drain();
-  __syncthreads();
-
-  // diagnostic timing (a.stamps != NULL, a separate measurement run): s_memtime per phase for
-  // blocks 0 and 128, every wave, the first 8 rounds -> stamps[((sel * 4 + w) * 8 + round) * 32 + point]
-  unsigned long long* stp = nullptr;
-  if (a.stamps && (blockIdx.x == 0 || blockIdx.x == 128))
-    stp = a.stamps + ((size_t)((blockIdx.x == 0 ? 0 : 1) * EB_WAVES + w) * 8) * 32;
-  int rcount = 0;
-#define EB_STAMP(k)                                                                      \
-  do {                                                                                  \
-    if (stp && rcount < 8 && lane0 == 0) stp[rcount * 32 + (k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-
-  for (int rd = first; rd < end; rd += step, ++rcount) {
-    EB_STAMP(0);
-    const int tile = rd * EB_WAVES + w;
-    const int mtile = tile < ntiles ? tile : ntiles - 1;
-    const int nrd = rd + step;
-    TiledTile xr, gn;  // next step's X image share; next round's G3 share
-
-    // ---------------------------------------------------------------- steps L = 3, 2, 1
-    auto layer_step = [&](auto Lc) {
-      constexpr int L = decltype(Lc)::value;
-      int lane = lane0;
-      asm volatile("" : "+v"(lane));  // per-step addresses: recompute, do not hoist
-      const int c = lane & 31, hl = lane >> 5;
-      const int lr = 32 * w + c;
-      const uint4* wcur = wbuf[L & 1];
-      glds_weights(wbuf[(L - 1) & 1], a.wtpk[L - 1], w, lane);  // W_{L-1}^T for the next step
-      if constexpr (L >= 2) {
-        xr.load(a.act[L - 2], tile, ntiles, a.rows, lane);  // X_{L-1} = a_{L-1}
-      } else if (nrd < end) {
-        xr.load(a.act[2], nrd * EB_WAVES + w, ntiles, a.rows, lane);  // next round: a3, G3
-        gn.load(a.g3, nrd * EB_WAVES + w, ntiles, a.rows, lane);
-      }
-      const uint32_t* mp = reinterpret_cast<const uint32_t*>(a.mask[L - 1]) + (size_t)mtile * 2 * 64 + lane;
-      const uint32_t mk0 = mp[0], mk1 = mp[64];
-      // dW_L[:, 32w..] += G_L^T X_L over the round's rows
-#pragma unroll 4
-      for (int ks = 0; ks < EB_ROUND / 16; ++ks) {
-        const int kb = 16 * ks + 8 * hl;
-        const int sub = 16 * ((lane >> 4) & 1);
-        const bf16x8 xb = tr8(xs, kb, 32 * w + sub, lane);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const bf16x8 ga = tr8(gs, kb, 32 * t + sub, lane);
-          dw[L - 1][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga, xb, dw[L - 1][t], 0, 0, 0);
-        }
-      }
-      EB_STAMP(1 + 5 * (3 - L));
-      // db_L partial: thread (rg, cq) sums rows 16rg..16rg+15 of features 4cq..4cq+3
-      {
-        const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-#pragma unroll 4
-        for (int r = 0; r < EB_ROUND / 8; ++r) {
-          const u32x2 x = get4(gs, 16 * rg + r, 4 * cq);
-          db[L - 1][0] += lo_bf16(x[0]);
-          db[L - 1][1] += hi_bf16(x[0]);
-          db[L - 1][2] += lo_bf16(x[1]);
-          db[L - 1][3] += hi_bf16(x[1]);
-        }
-      }
-      // chain: G_{L-1} = (G_L W_L) . [a_L > 0], rows on lanes (the k-step / tile order of
-      // common.hpp gemm(): bitwise the split path's pre-activation gradients)
-      f32x16 acc[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
-#pragma unroll 4
-      for (int u = 0; u < 8; ++u) {
-        const bf16x8 b = brow(gs, lr, u, hl);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const bf16x8 wa = __builtin_bit_cast(bf16x8, wcur[(t * 8 + u) * 64 + lane]);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b, acc[t], 0, 0, 0);
-        }
-      }
-      EB_STAMP(2 + 5 * (3 - L));
-      __syncthreads();  // every read of the G / X images and of W_L is done
-      EB_STAMP(3 + 5 * (3 - L));
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const uint32_t mk = (t < 2) ? mk0 : mk1;  // register 16t + r -> dword t >> 1, bit 16 (t & 1) + r
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int bit = 16 * (t & 1) + 4 * q + e;
-            v[e] = __uint_as_float(__float_as_uint(acc[t][4 * q + e]) & (uint32_t)__builtin_amdgcn_sbfe((int32_t)mk, bit, 1));
-          }
-          put4(gs, lr, 32 * t + 8 * q + 4 * hl, pack2(v[0], v[1]), pack2(v[2], v[3]));
-        }
-      }
-      if constexpr (L >= 2) xr.store(xs, w, lane);
-      vm_drain();  // W_{L-1}^T has landed
-      EB_STAMP(4 + 5 * (3 - L));
-      __syncthreads();
-      EB_STAMP(5 + 5 * (3 - L));
-    };
-    layer_step(std::integral_constant<int, 3>{});
-    layer_step(std::integral_constant<int, 2>{});
-    layer_step(std::integral_constant<int, 1>{});
-
-    // ---------------------------------------------------------------- step 0: de, G0
-    {
-      int lane = lane0;
-      asm volatile("" : "+v"(lane));
-      const int c = lane & 31, hl = lane >> 5;
-      const int lr = 32 * w + c;
-      const int row = tile * 32 + c;
-      const bool valid = tile < ntiles && row < a.rows;
-      const int rr = valid ? row : a.rows - 1;
-      if (nrd < end) {
-        glds_weights(wbuf[1], a.wtpk[3], w, lane);  // next round's W3^T
-        xr.store(xs, w, lane);                      // X image is free in step 0 (dW_e is not fused)
-      }
-      RowTile g1, g2;  // residual: dL/de' = g + g2[dst]
-      if (a.g) g1.load(reinterpret_cast<const bf16*>(a.g) + (size_t)rr * H, lane);
-      else g1.zero();
-      g2.load(reinterpret_cast<const bf16*>(a.g2) + (size_t)a.gidx[rr] * H, lane);
-      f32x16 acc[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
-      const uint4* wcur = wbuf[0];
-#pragma unroll 4
-      for (int u = 0; u < 8; ++u) {
-        const bf16x8 b = brow(gs, lr, u, hl);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const bf16x8 wa = __builtin_bit_cast(bf16x8, wcur[(t * 8 + u) * 64 + lane]);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b, acc[t], 0, 0, 0);
-        }
-      }
-      EB_STAMP(16);
-      // de = G0 W_e + (g + g2): acc registers 8i..8i+7 = acc[i >> 1][8 (i & 1) + e]
-      bf16* dep = reinterpret_cast<bf16*>(a.de) + (size_t)rr * H;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float v[8], x[8], y[8];
-        unpack8_w(x, g1.v[i]);
-        unpack8_w(y, g2.v[i]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = acc[i >> 1][8 * (i & 1) + e] + (x[e] + y[e]);
-        store8_w(dep, i, hl, v, valid);
-      }
-      // G0 tile -> HBM (16-B chunks of the own rows of the G image), then the next round's G3
-      bf16* g0 = reinterpret_cast<bf16*>(a.g0) + (size_t)tile * 32 * H;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int q = lane + 64 * k, r = q >> 4, ch = q & 15;
-        const u32x2 lo = get4(gs, 32 * w + r, 8 * ch), hi = get4(gs, 32 * w + r, 8 * ch + 4);
-        if (tile < ntiles && tile * 32 + r < a.rows)
-          *reinterpret_cast<uint4*>(g0 + (size_t)r * H + 8 * ch) = __builtin_bit_cast(uint4, u32x4{lo[0], lo[1], hi[0], hi[1]});
-      }
-      if (nrd < end) gn.store(gs, w, lane);  // only this wave ever reads its rows in step 0
-      EB_STAMP(17);
+      for (int y = 0; y < 2; ++y) dw[l][x][y] = f32x16{};
     }
-    vm_drain();       // next round's W3^T has landed
-    EB_STAMP(18);
-    __syncthreads();
-    EB_STAMP(19);
+  int n = 0;
+#ifdef AGN_EB_STAMPS
+  unsigned long long waited = 0;
+  const unsigned long long tstart = __builtin_amdgcn_s_memtime();
+#endif
+  for (int rd = rw.first; rd < rw.end; rd += rw.step) {
+    const int cmax = min(CW, ntiles - rd * CW);
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int li = s >> 1;  // 0: L = 3, 1: L = 2, 2: L = 1
+      for (int cc = 0; cc < cmax; ++cc, ++n) {
+        const int k = n % NSLOT, j = n / NSLOT;
+#ifdef AGN_EB_STAMPS
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        wait_ge(&filled[k], j + 1);
+        waited += __builtin_amdgcn_s_memtime() - t0;
+#else
+        wait_ge(&filled[k], j + 1);
+#endif
+        const char* sb = lds + OFF_RING + k * SLOT_B;
+        const bf16x8 g0 = tr_pair(sb + 512 * ob + t1, sb + 512 * ob + t2);
+        const bf16x8 g1 = tr_pair(sb + 512 * (ob + 1) + t1, sb + 512 * (ob + 1) + t2);
+        const bf16x8 x0 = tr_pair(sb + HALF_B + 512 * ib + t1, sb + HALF_B + 512 * ib + t2);
+        const bf16x8 x1 = tr_pair(sb + HALF_B + 512 * (ib + 1) + t1, sb + HALF_B + 512 * (ib + 1) + t2);
+        lgkm_drain();
+        if (lane == 0) __hip_atomic_fetch_add(&consumed[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        mfma(dw[li][0][0], g0, x0);
+        mfma(dw[li][0][1], g0, x1);
+        mfma(dw[li][1][0], g1, x0);
+        mfma(dw[li][1][1], g1, x1);
+        if ((d & 1) == 0) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            dbs[li][0] += (float)g0[e];
+            dbs[li][1] += (float)g1[e];
+          }
+        }
+      }
+    }
   }
-#undef EB_STAMP
-
-  // ---------------------------------------------------------------- per-block partials
-  const int lane = lane0, c = lane0 & 31, hl = lane0 >> 5;
+#ifdef AGN_EB_STAMPS
+  if (a.stamps && (blockIdx.x == 0 || blockIdx.x == 128) && lane == 0) {
+    unsigned long long* sp = a.stamps + ((blockIdx.x == 0 ? 0 : 8) + 4 + d) * 8 * 16;
+    sp[0] = waited;
+    sp[1] = __builtin_amdgcn_s_memtime() - tstart;
+    sp[2] = (unsigned long long)n;
+  }
+#endif
+  // partial slabs (true feature order): dW_L of workgroup b at dw_partial[(L-1) nblk + b][o][i]
   const size_t slab = (size_t)H * H;
 #pragma unroll
-  for (int l = 0; l < 3; ++l) {
-    float* P = a.dw_partial + ((size_t)l * a.nblk + blockIdx.x) * slab;
+  for (int li = 0; li < 3; ++li) {
+    float* Pw = a.dw_partial + ((size_t)(2 - li) * a.nblk + blockIdx.x) * slab;
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = 32 * t + 8 * (r >> 2) + 4 * hl + (r & 3);
-        P[(size_t)m * H + 32 * w + c] = dw[l][t][r];
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int op = 32 * (ob + x) + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const int ip = 32 * (ib + y) + (lane & 31);
+          Pw[(size_t)phi(op) * H + phi(ip)] = dw[li][x][y][r];
+        }
+    if ((d & 1) == 0) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        const float t = dbs[li][x] + __shfl_xor(dbs[li][x], 32, 64);  // rows 8hh.. of both halves
+        if (hh == 0) a.db_partial[((size_t)(2 - li) * a.nblk + blockIdx.x) * H + phi(32 * (ob + x) + lane)] = t;
       }
+    }
   }
-  // db: 8 row groups per column quad, summed in group order through the (now free) X image
-  float* red = reinterpret_cast<float*>(xs);  // [3][8][128] floats = 12 KB
-  {
-    const int cq = threadIdx.x & 31, rg = threadIdx.x >> 5;
-#pragma unroll
-    for (int l = 0; l < 3; ++l)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) red[(l * 8 + rg) * H + 4 * cq + e] = db[l][e];
+}
+
+__global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_bwd_args a) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_B];
+  // weight images from the packed forward operands: unit (ot, ku, lane) -> row 32ot + lane%32,
+  // chunk 2ku + lane/32
+  for (int l = 0; l < 4; ++l) {
+    const uint4* src = reinterpret_cast<const uint4*>(a.wpk[l]);
+    for (int u = threadIdx.x; u < 2048; u += NTHR) {
+      const int ln = u & 63, unit = u >> 6;
+      const int o = 32 * (unit >> 3) + (ln & 31), ch = 2 * (unit & 7) + (ln >> 5);
+      *reinterpret_cast<uint4*>(lds + l * IMG_B + aoff(o, ch)) = src[u];
+    }
   }
-  __syncthreads();
-  (void)lane;
-  for (int i = threadIdx.x; i < 3 * H; i += EB_THREADS) {
+  float* pv = reinterpret_cast<float*>(lds + OFF_PV);
+  for (int i = threadIdx.x; i < 4 * H; i += NTHR) {
     const int l = i / H, f = i - l * H;
+    pv[i] = l < 3 ? (a.bias[l + 1] ? a.bias[l + 1][f] : 0.f) : a.ln_g[f];
+  }
+  if (threadIdx.x < 8) reinterpret_cast<int*>(lds + OFF_FLAG)[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < CW * 2 * H; i += NTHR) reinterpret_cast<float*>(lds + OFF_LNP)[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wave < CW) chain_wave(a, lds, wave, lane);
+  else dw_wave(a, lds, wave - CW, lane);
+  __syncthreads();
+  // LayerNorm parameter partials of the four chain waves, summed in wave order
+  const float* lnp = reinterpret_cast<const float*>(lds + OFF_LNP);  // [CW][2][H]
+  for (int i = threadIdx.x; i < 2 * H; i += NTHR) {
     float s = 0.f;
-    for (int rg = 0; rg < 8; ++rg) s += red[(l * 8 + rg) * H + f];
-    a.db_partial[((size_t)l * a.nblk + blockIdx.x) * H + f] = s;
+#pragma unroll
+    for (int w = 0; w < CW; ++w) s += lnp[w * 2 * H + i];
+    a.ln_partial[(size_t)blockIdx.x * 2 * H + i] = s;
   }
 }
 
@@ -389,21 +657,19 @@ int agn_edge_bwd_blocks(int rows) {
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) g_cus = pr.multiProcessorCount;
     if (g_cus <= 0) g_cus = 256;
   }
-  const int rounds = ((rows + 31) / 32 + 3) / 4;
+  const int rounds = ((rows + 31) / 32 + CW - 1) / CW;
   if (rounds >= g_cus) return g_cus;
   const int n = (rounds + 7) / 8 * 8;
   return n < 8 ? 8 : n;
 }
 
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
-  if (!a || a->rows < 1 || a->nblk < 1 || !a->g2 || !a->gidx || !a->g3 || !a->de || !a->g0 || !a->dw_partial ||
-      !a->db_partial)
+  if (!a || a->rows < 1 || a->nblk < 1 || !a->e || !a->proj || !a->src || !a->dst || !a->g2 || !a->ln_g ||
+      !a->de || !a->g0 || !a->dw_partial || !a->db_partial || !a->ln_partial)
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
-    if (!a->wtpk[l]) return AGN_E_ARG;
-  for (int l = 0; l < 3; ++l)
-    if (!a->act[l] || !a->mask[l]) return AGN_E_ARG;
-  hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(EB_THREADS), 0, (hipStream_t)stream, *a);
+    if (!a->wpk[l]) return AGN_E_ARG;
+  hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

@@ -281,7 +281,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
         const float d = acc[i / 16][i % 16] - mean;
-        q += (OUT_FULL || feat_of(i, h) < outd) ? d * d : 0.f;
+        if (OUT_FULL || feat_of(i, h) < outd) q = ln_sq_acc(q, d);
       }
       q += xor32(q);
       rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
@@ -430,9 +430,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       for (int e = 0; e < 4; ++e) {
         const bool in = VEC || f0 + e < M;
         const float xh = in ? (hv[e] - mean) * rstd : 0.f;
-        const float gg = A[4 * q + e] * gm[e];
-        c1 += gg;
-        c2 += gg * xh;
+        ln_bwd_acc(c1, c2, A[4 * q + e], gm[e], xh);
         B[4 * q + e] = A[4 * q + e] * xh;  // g * xhat (LN weight-grad partial)
       }
     }
@@ -471,7 +469,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       for (int e = 0; e < 4; ++e) {
         const bool in = VEC || f0 + e < M;
         const float xh = (hv[e] - mean) * rstd;
-        A[4 * q + e] = in ? (A[4 * q + e] * gm[e] - c1 - xh * c2) * rstd : 0.f;
+        A[4 * q + e] = in ? ln_bwd_out(A[4 * q + e], gm[e], c1, c2, xh, rstd) : 0.f;
       }
     }
   }
@@ -680,7 +678,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int i = 0; i < NR; ++i) {
         const float d = acc[i / 16][i % 16] - mean;
-        q += d * d;
+        q = ln_sq_acc(q, d);
       }
       q += xor32(q);
       rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
@@ -844,9 +842,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
           for (int e = 0; e < 4; ++e) {
             const int r = 8 * i + 4 * j + e;
             const float xh = (hv[4 * j + e] - mean) * rstd;
-            const float gg = A[r] * gm[e];
-            c1 += gg;
-            c2 += gg * xh;
+            ln_bwd_acc(c1, c2, A[r], gm[e], xh);
             B[r] = A[r] * xh;
           }
         }
@@ -876,6 +872,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
           for (int e = 0; e < 4; ++e) {
             const int r = 8 * i + 4 * j + e;
             const float xh = (hv[4 * j + e] - mean) * rstd;
+            // (= ln_bwd_out: hipcc emits fma(A, gm, -c1), fma(-xh, c2, .), * rstd here; the explicit
+            // helper makes this kernel spill 19 registers, so the expression stays)
             A[r] = (A[r] * gm[e] - c1 - xh * c2) * rstd;
           }
         }

@@ -323,32 +323,37 @@ int agn_wec_blocks(int n);
 int agn_wec_forward(const agn_wec_args* a, void* stream);
 int agn_wec_backward(const agn_wec_args* a, void* stream);
 
-/* ---- fused edge-MLP backward with in-kernel weight gradients (bf16, H = 128, the sum-trick
- * EdgeBlockSum chain h0 = e W_e^T + P_s[src] + P_d[dst] -> ReLU -> Lin1 -> ReLU -> Lin2 -> ReLU
- * -> Lin3 -> LayerNorm, mgnLayer.py:72-105, and the residual e' = e + ., mgnLayer.py:205).
- * Replaces the chain part of agn_mlp_backward + agn_wgrad for that chain: given G3 = dL/dh3 (the
- * LayerNorm backward, agn_mlp_backward with nlin = 1), one persistent launch runs the chain rule
- * through Lin3..Lin1 and W_e and accumulates dW1..dW3 / db1..db3 in registers, so the
- * pre-activation gradients G1, G2 are never written and G3 / the activations are read once.
- * Outputs: de (with the residual gradient g + g2[gidx]), G0 = dL/dh0 (row-major; its sender /
+/* ---- fused training backward of the sum-trick edge MLP with forward recompute and in-kernel
+ * weight gradients (bf16, H = 128; the EdgeBlockSum chain h0 = e W_e^T + P_s[src] + P_d[dst] ->
+ * ReLU -> Lin1 -> ReLU -> Lin2 -> ReLU -> Lin3 -> LayerNorm, mgnLayer.py:72-105, and the residual
+ * e' = e + ., mgnLayer.py:205). Replaces agn_mlp_backward + the chain's agn_wgrad share for that
+ * chain, and lets the training forward save nothing: one persistent launch recomputes h0..h3
+ * from e and the projection rows (bitwise the forward kernel's values), runs the LayerNorm
+ * backward and the chain rule, and accumulates dW1..dW3 / db1..db3 on chip, so no activation and
+ * no pre-activation gradient but G0 ever reaches HBM.
+ * Outputs: de (with the residual gradient g + g2[dst]), G0 = dL/dh0 (row-major; its sender /
  * receiver segment sums are dP_s / dP_d, and dW_e = G0^T e goes to agn_wgrad), and per-block
- * partials that agn_wgrad_reduce sums in fixed order. de and G0 are bitwise those of the split
- * path; dW / db differ from it only in the fp32 order of the row sums. ---- */
+ * partials (dW, db: agn_wgrad_reduce; LayerNorm: agn_colsum) summed in fixed order. de and G0
+ * are bitwise those of the split path; dW / db / LayerNorm grads differ from it only in the fp32
+ * order of the row sums. ---- */
 typedef struct {
   int rows;                  /* edges (CSC order) */
-  int nblk;                  /* grid size: agn_edge_bwd_blocks() */
-  const void* wtpk[4];       /* packed A = W_l^T of W_e, Lin1, Lin2, Lin3 (agn_pack, bf16) */
+  int nblk;                  /* grid size: agn_edge_bwd_blocks(rows) */
+  const void* wpk[4];        /* packed A = W_l of W_e, Lin1, Lin2, Lin3 (agn_pack trans = 0, bf16) */
+  const float* bias[4];      /* fp32 biases; bias[1..3] of Lin1..Lin3 (bias[0] unused: W_e has none) */
+  const float* ln_g;         /* LayerNorm gamma [128] */
+  const void* e;             /* [rows][128] the layer's edge input (CSC order) */
+  const void* proj;          /* [N][256] P = [x W_s^T | x W_d^T + b] of the forward */
+  const int32_t* src;        /* [rows] sender of each edge */
+  const int32_t* dst;        /* [rows] receiver of each edge (row of proj's P_d half and of g2) */
   const void* g;             /* [rows][128] grad of e' or NULL (unused output) */
   const void* g2;            /* [N][128] dAgg (receiver-side grad) */
-  const int32_t* gidx;       /* [rows] receiver of each edge (row of g2) */
-  const void* g3;            /* AGN_TILED dL/dh3 (LayerNorm backward output) */
-  const void* act[3];        /* AGN_TILED a1, a2, a3 (ReLU outputs = inputs of Lin1..Lin3) */
-  const void* mask[3];       /* their AGN_RELU_MASK bits */
   void* de;                  /* [rows][128] out: dL/de incl. the residual */
   void* g0;                  /* [rows][128] out: dL/dh0 */
   float* dw_partial;         /* [3][nblk][128][128]: dW1..dW3 slabs (agn_wgrad slab order) */
   float* db_partial;         /* [3][nblk][128] */
-  unsigned long long* stamps; /* diagnostics only: NULL, or [2][4][8][32] s_memtime per phase */
+  float* ln_partial;         /* [nblk][2][128]: sum g * xhat, sum g (LayerNorm weight / bias grads) */
+  unsigned long long* stamps; /* diagnostics only (a -DAGN_EB_STAMPS build): NULL, or [2][8][8][16] */
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
@@ -369,14 +374,16 @@ int agn_proj_backward(int rows, const void* dps, const void* dpd, int dp_ld, con
 
 /* ---- device data preparation (dataset.py:39-106, :358-409; train.py:50-51) ----
  * agn_edge_features: out[i] = [pos[dst]-pos[src], |pos[dst]-pos[src]|] of edge e = perm ? perm[i] : i
- *   (edge_index int64 [2][ne]), optionally normalised (v - mean) / std per column; [ne][pdim + 1] fp32.
+ *   (i < ne output rows; edge_index int64 [2][e_total], perm int64), optionally normalised
+ *   (v - mean) / std per column; [ne][pdim + 1] fp32.
  * agn_normalize: out = (x - mean) / std per column (inverse: x * std + mean, denormalize_predictions).
- * agn_col_stats: torch.std_mean(x, dim=0) (unbiased) of an [n][k] fp32 matrix, std clamped >= eps;
+ * agn_col_stats: torch.std_mean(x, dim=0) (unbiased: NaN std for n = 1) of an [n][k] fp32 matrix, std clamped
+ *   >= eps as torch.clamp does (a NaN stays NaN);
  *   deterministic fp64 two-pass; scratch = agn_col_stats_temp_bytes(n, k).
  * agn_collate: PyG Batch of B meshes concatenated row-wise: edge_index (in place) += the node offset
  *   of each edge's mesh, batch[v] = mesh of node v; edge_off / node_off exclusive prefix sums [B + 1]. */
-int agn_edge_features(int ne, int pdim, const int64_t* edge_index, const float* pos, int pos_ld, const int64_t* perm,
-                      const float* mean, const float* std, float* out, void* stream);
+int agn_edge_features(int ne, int64_t e_total, int pdim, const int64_t* edge_index, const float* pos, int pos_ld,
+                      const int64_t* perm, const float* mean, const float* std, float* out, void* stream);
 int agn_normalize(int n, int k, const float* x, int ld, const float* mean, const float* std, float* out, int out_ld,
                   int inverse, void* stream);
 size_t agn_col_stats_temp_bytes(int n, int k);

@@ -260,9 +260,10 @@ def test_relu_mask_matches_saved_activations(rows, dtype):
 
 @pytest.mark.parametrize("E", [98_400, 70_001])  # ragged last round / ragged last tile
 def test_fused_edge_bwd_matches_split(E, monkeypatch):
-    """agn_edge_bwd_fused (LayerNorm backward pass + one persistent chain/dW kernel) against the
-    split path (agn_mlp_backward + agn_wgrad): activations, dx and de bitwise equal (same MFMA
-    order per row), parameter gradients equal up to the fp32 order of the row sums."""
+    """agn_edge_bwd_fused (forward recompute + LayerNorm backward + chain rule + dW1..dW3 in one
+    persistent launch; the forward saves nothing) against the split path (saved activations,
+    agn_mlp_backward + agn_wgrad): outputs, dx and de bitwise equal (same operands and MFMA order
+    per row), parameter gradients equal up to the fp32 order of the row sums."""
     from aerognn.graph import Level
     from models.mgnLayer import MeshGraphNetLayer
     m = _mesh(150, 110)

@@ -1,39 +1,83 @@
 """Phase clocks of agn_edge_bwd_fused (diagnostic run, not the product path): one C3 level-0
-MeshGraphNetLayer fwd+bwd with core.STAMPS set; prints the median cycles per phase per round."""
+sized layer (1M nodes / ~6M edges), the -DAGN_EB_STAMPS library (AEROGNN_LIB), s_memtime per
+phase of the chain waves of blocks 0 and 128 (8 tiles each) and the dW waves' wait share.
+
+Usage (GPU): AEROGNN_LIB=aero-gnn_amd/aerognn/libaerognn_stamps.so python tools/edge_bwd_stamps.py
+"""
 import os
 import sys
-
-import numpy as np
-import torch
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "aero-gnn_amd")]
+sys.path.insert(0, os.path.join(ROOT, "aero-gnn_amd"))
+sys.path.insert(0, ROOT)
 os.environ.setdefault("AEROGNN_MEMLOG", "0")
-from aerognn import core  # noqa: E402
-from aerognn.graph import Level  # noqa: E402
-from aerognn.meshgen import ellipsoid  # noqa: E402
-from models.mgnLayer import MeshGraphNetLayer  # noqa: E402
 
-m = ellipsoid(1000, 1000)
-ei = torch.from_numpy(m["edge_index"]).cuda()
-N, E = m["x"].shape[0], ei.shape[1]
-lv = Level.from_edge_index(ei, N)
-torch.manual_seed(0)
-layer = MeshGraphNetLayer(128, 128, 128, 2, 2, do_concat_trick=True).cuda()
-x = torch.randn(N, 128, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
-e = torch.randn(E, 128, device="cuda", dtype=torch.bfloat16).requires_grad_(True)
-for it in range(3):
-    core.STAMPS = torch.zeros(2 * 4 * 8 * 32, dtype=torch.int64, device="cuda") if it == 2 else None
-    xo, eo = layer.forward_level(x, e, lv)
-    (xo.float().sum() + eo.float().sum()).backward()
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PHASES = ["ids+loads", "forward", "LN stats+bwd", "recompute a2,a3", "produce L3", "chain L3", "produce L2",
+          "chain L2", "produce L1", "chain L1", "step 0 (de, G0)"]
+
+
+def main():
+    from aerognn import core
+    from aerognn.graph import Level
+    from aerognn.meshgen import ellipsoid
+    from models.mgnLayer import MeshGraphNetLayer
+    dev = "cuda"
+    nu = int(os.environ.get("NU", "1000"))
+    m = ellipsoid(nu, nu, seed=0)
+    ei = torch.from_numpy(np.ascontiguousarray(m["edge_index"])).to(dev)
+    N, E, H = m["x"].shape[0], ei.shape[1], 128
+    torch.manual_seed(0)
+    layer = MeshGraphNetLayer(128, 128, 128, 2, 2, do_concat_trick=True).to(dev)
+    lv = Level.from_edge_index(ei, N)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    dt = torch.bfloat16
+    x = torch.randn(N, H, generator=g).to(dev, dt)
+    e = torch.randn(E, H, generator=g).to(dev, dt)
+    ge = torch.randn(E, H, generator=g).to(dev, dt)
+    dagg = torch.randn(N, H, generator=g).to(dev, dt)
+    spec = layer.spec()
+    spec.pack.update(dt, dev)
+    es = spec.edge
+    P = torch.empty(N, 2 * H, dtype=dt, device=dev)
+    core.proj_forward(N, x, spec.pack["proj"], spec.pack["proj_b"], P)
+    de = torch.empty_like(e)
+    g0 = torch.empty(E, H, dtype=dt, device=dev)
+
+    def run():
+        return core.edge_bwd_fused(rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
+                                   src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de, g0=g0)
+    for _ in range(3):
+        run()
     torch.cuda.synchronize()
-st = core.STAMPS.cpu().numpy().reshape(2, 4, 8, 32).astype(np.int64)
-names = ["start"] + [f"L{L}:{k}" for L in (3, 2, 1) for k in ("dW", "chain", "barB", "drain", "barA")] + \
-        ["s0:chain", "s0:stores", "s0:drain", "s0:bar"]
-pts = [0] + [1 + 5 * (3 - L) + k for L in (3, 2, 1) for k in range(5)] + [16, 17, 18, 19]
-d = np.diff(st[:, :, 1:7, pts], axis=-1)  # rounds 1..6 (skip the first)
-med = np.median(d.reshape(-1, d.shape[-1]), axis=0)
-for n, v in zip(names[1:], med):
-    print(f"{n:10s} {v:8.0f}")
-tot = np.median((st[:, :, 2:7, 0] - st[:, :, 1:6, 0]).reshape(-1))
-print(f"round total {tot:.0f} cycles")
+    t = time.perf_counter()
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    print(f"E = {E}: {1e3 * (time.perf_counter() - t) / 5:.3f} ms per launch (incl. the slab reduce)")
+    core.STAMPS = torch.zeros(2 * 8 * 8 * 16, dtype=torch.int64, device=dev)
+    run()
+    torch.cuda.synchronize()
+    st = core.STAMPS.cpu().numpy().reshape(2, 8, 8, 16).astype(np.int64)
+    core.STAMPS = None
+    for sel in range(2):
+        print(f"block {0 if sel == 0 else 128}:")
+        tot = np.zeros(len(PHASES))
+        for w in range(4):
+            s = st[sel, w]
+            d = np.diff(s[1:8, :12], axis=1)  # tiles 1..7, phases 0..11
+            tot += d.mean(0)
+            per_tile = (s[2:8, 0] - s[1:7, 0]).mean()
+            print(f"  chain wave {w}: cycles/tile {per_tile:9.0f}   " +
+                  " ".join(f"{x:6.0f}" for x in d.mean(0)))
+        print("  phases (mean over waves): " + ", ".join(f"{p} {v / 4:.0f}" for p, v in zip(PHASES, tot)))
+        for dwv in range(4):
+            s = st[sel, 4 + dwv]
+            print(f"  dW wave {dwv}: waited {s[0, 0]} of {s[0, 1]} cycles ({s[0, 0] / max(s[0, 1], 1):.2f}), items {s[0, 2]}")
+
+
+if __name__ == "__main__":
+    main()
