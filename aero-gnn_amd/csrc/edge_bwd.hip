@@ -185,29 +185,43 @@ struct Rounds {  // XCD-grouped round walk (blocks b and b + 8 share an XCD and 
 };
 
 // ------------------------------------------------------------------------------ chain wave
-// Item n = (round, s = 2 (3 - L) + half, chain wave): G_L and a_L of rows 16 half .. 16 half + 15
-// of the wave's tile, as two layout (a) images: unit i of lane (c, hh) = positions 16i + 8hh..+7
-// (chunk 2i + hh) of row c & 15.
-AGN_DEV void produce(char* lds, int n, const BOp<bf16, NR>& G, const BOp<bf16, NR>& X, int half, int lane) {
+// Item n = (round, L, chain wave, half), n = 24 round + 8 (3 - L) + 2 cw + half: G_L and a_L of
+// rows 16 half .. 16 half + 15 of the wave's tile, as two layout (a) images: unit i of lane
+// (c, hh) = positions 16i + 8hh..+7 (chunk 2i + hh) of row c & 15. A chain wave hands both halves
+// over at once (items n0, n0 + 1): every lane writes, each half into its own slot.
+AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<bf16, NR>& X, int lane,
+                          unsigned long long* ist = nullptr) {
   int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
   int* consumed = filled + 4;
-  const int k = n % NSLOT, j = n / NSLOT;
-  wait_ge(&consumed[k], 4 * j);
+  const int k0 = n0 % NSLOT, j0 = n0 / NSLOT;
+  const int k1 = (n0 + 1) % NSLOT, j1 = (n0 + 1) / NSLOT;
+#ifdef AGN_EB_STAMPS
+  if (ist && lane == 0) ist[0] = __builtin_amdgcn_s_memtime();
+#endif
+  wait_ge(&consumed[k0], 4 * j0);
+  wait_ge(&consumed[k1], 4 * j1);
+#ifdef AGN_EB_STAMPS
+  if (ist && lane == 0) ist[1] = __builtin_amdgcn_s_memtime();
+#endif
   const int c = lane & 31, hh = lane >> 5;
-  if ((c >> 4) == half) {
-    char* sb = lds + OFF_RING + k * SLOT_B;
-    const int r = c & 15, x = (r >> 2) & 3;
-    const int base = 2048 * (r >> 3) + 64 * (r & 7);
-    const int oe = base + 16 * (hh ^ x), oo = base + 16 * ((2 + hh) ^ x);  // aoff(r, 2i + hh), i even / odd
+  char* sb = lds + OFF_RING + ((c >> 4) ? k1 : k0) * SLOT_B;
+  const int r = c & 15, x = (r >> 2) & 3;
+  const int base = 2048 * (r >> 3) + 64 * (r & 7);
+  const int oe = base + 16 * (hh ^ x), oo = base + 16 * ((2 + hh) ^ x);  // aoff(r, 2i + hh), i even / odd
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int o = (i & 1 ? oo : oe) + 512 * (i >> 1);
-      *reinterpret_cast<uint4*>(sb + o) = __builtin_bit_cast(uint4, G.u[i]);
-      *reinterpret_cast<uint4*>(sb + HALF_B + o) = __builtin_bit_cast(uint4, X.u[i]);
-    }
+  for (int i = 0; i < 8; ++i) {
+    const int o = (i & 1 ? oo : oe) + 512 * (i >> 1);
+    *reinterpret_cast<uint4*>(sb + o) = __builtin_bit_cast(uint4, G.u[i]);
+    *reinterpret_cast<uint4*>(sb + HALF_B + o) = __builtin_bit_cast(uint4, X.u[i]);
   }
   lgkm_drain();
-  if (lane == 0) __hip_atomic_store(&filled[k], j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (lane == 0) {
+    __hip_atomic_store(&filled[k0], j0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&filled[k1], j1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+#ifdef AGN_EB_STAMPS
+  if (ist && lane == 0) ist[2] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 // G_{L-1} = dA . [a_L > 0] (the split path's AGN_RELU_MASK select, from the packed activation)
@@ -225,10 +239,15 @@ AGN_DEV void relu_select(float (&A)[NR], const f32x16 (&acc)[NT], const BOp<bf16
   do {                                                                                                  \
     if (stp && ntile_done < 8 && (lane0 & 63) == 0) stp[ntile_done * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// item-level clocks of produce(): tiles 1 and 2 of block 0's chain waves, at 2048 + 576 + ..
+#define EB_IST(pi) \
+  ((stp && blockIdx.x == 0 && (ntile_done == 1 || ntile_done == 2)) \
+       ? a.stamps + 2048 + 576 + ((cw * 2 + ntile_done - 1) * 6 + (pi)) * 3 : nullptr)
 #else
 #define EB_STAMP(k) \
   do {              \
   } while (0)
+#define EB_IST(pi) nullptr
 #endif
 
 AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0) {
@@ -243,6 +262,16 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   const float* pv = reinterpret_cast<const float*>(lds + OFF_PV);
   const bf16* P = reinterpret_cast<const bf16*>(a.proj);
   int rcount = 0;
+  // the node ids of a wave's next tile are loaded one tile ahead: the tile's P_s / P_d gathers
+  // then wait for one memory latency instead of two dependent ones
+  auto tile_ids = [&](int rd, int& sid, int& did) {
+    const int row = (rd * CW + cw) * 32 + (lane0 & 31);
+    const int rr = row < a.rows ? row : a.rows - 1;
+    sid = a.src[rr];
+    did = a.dst[rr];
+  };
+  int sid_next = 0, did_next = 0;
+  if (rw.first < rw.end) tile_ids(rw.first, sid_next, did_next);
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
     if (cw >= cmax) continue;
@@ -257,9 +286,15 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
-    const int sid = a.src[rr], did = a.dst[rr];
-    // incoming gradient row g: loaded now, kept raw (32 registers) through the forward recompute
-    uint4 graw[NR / 8];
+    const int sid = sid_next, did = did_next;
+    // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
+    // forward recompute
+    uint4 graw[NR / 8], g2raw[NR / 8];
+    {
+      const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) g2raw[i] = *reinterpret_cast<const uint4*>(g2p + 16 * i + 8 * h);
+    }
     if (a.g) {
       const bf16* gp = reinterpret_cast<const bf16*>(a.g) + (size_t)rr * H;
 #pragma unroll
@@ -345,13 +380,12 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     float A[NR];
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
-      float o[8];
+      float o[8], o2[8];
       unpack8_w(o, graw[i]);  // load8_w's exchange + conversion
+      unpack8_w(o2, g2raw[i]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) A[8 * i + e] = o[e];
+      for (int e = 0; e < 8; ++e) A[8 * i + e] = o[e] + o2[e];
     }
-    sched_fence();
-    add_row_w<bf16, NR>(A, reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H, h);
     if (!valid) {
 #pragma unroll
       for (int i = 0; i < NR; ++i) A[i] = 0.f;
@@ -446,8 +480,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       pin(a3);
       sched_fence();
       EB_STAMP(4);
-      produce(lds, nbase + 0 * cmax + cw, op, a3, 0, fresh_lane(lane));
-      produce(lds, nbase + 1 * cmax + cw, op, a3, 1, fresh_lane(lane));
+      produce_pair(lds, nbase + 0 * cmax + 2 * cw, op, a3, fresh_lane(lane), EB_IST(0));
       EB_STAMP(5);
       gemm_cols(acc, op, lds + 3 * IMG_B, fresh_lane(lane));
       relu_select(A, acc, a3);
@@ -456,8 +489,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     op.set(A);  // G2
     pin(op);
-    produce(lds, nbase + 2 * cmax + cw, op, a2, 0, fresh_lane(lane));
-    produce(lds, nbase + 3 * cmax + cw, op, a2, 1, fresh_lane(lane));
+    produce_pair(lds, nbase + 2 * cmax + 2 * cw, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
     relu_select(A, acc, a2);
@@ -465,8 +497,23 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     op.set(A);  // G1
     pin(op);
-    produce(lds, nbase + 4 * cmax + cw, op, a1, 0, fresh_lane(lane));
-    produce(lds, nbase + 5 * cmax + cw, op, a1, 1, fresh_lane(lane));
+    // de = G0 W_e + (g + g2) (mlp_bwd_res_kernel's add_grad_w order) needs the incoming rows
+    // again: re-read now (L2) so the loads complete under the L1 hand-off and chain step.
+    // Opaque indices keep the compiler from holding the first reads' values live since the LN.
+    {
+      int did2 = did, rr2 = rr;
+      opaque(did2);
+      opaque(rr2);
+      const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did2 * H;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) g2raw[i] = *reinterpret_cast<const uint4*>(g2p + 16 * i + 8 * h);
+      if (a.g) {
+        const bf16* gp = reinterpret_cast<const bf16*>(a.g) + (size_t)rr2 * H;
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
+      }
+    }
+    produce_pair(lds, nbase + 4 * cmax + 2 * cw, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
     gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
     relu_select(A, acc, a1);
@@ -476,31 +523,22 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     pin(op);
     op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
-    // de = G0 W_e + (g + g2): mlp_bwd_res_kernel's add_grad_w order. The rows are re-read (L2):
-    // opaque indices keep the compiler from holding the first reads' values live since the LN
     {
       float v[NR];
 #pragma unroll
-      for (int i = 0; i < NR; ++i) v[i] = acc[i / 16][i % 16];
-      int did2 = did, rr2 = rr;
-      opaque(did2);
-      opaque(rr2);
-      const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did2 * H;
-      if (a.g) {
-        const bf16* g1p = reinterpret_cast<const bf16*>(a.g) + (size_t)rr2 * H;
+      for (int i = 0; i < NR / 8; ++i) {
+        float x[8], y[8];
+        unpack8_w(x, graw[i]);
+        unpack8_w(y, g2raw[i]);
 #pragma unroll
-        for (int i = 0; i < NR / 8; ++i) {
-          float x[8], y[8];
-          load8_w(x, g1p, i, h);
-          load8_w(y, g2p, i, h);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * i + e] += x[e] + y[e];
+        for (int e = 0; e < 8; ++e) {
+          const float t = acc[(8 * i + e) / 16][(8 * i + e) % 16];
+          v[8 * i + e] = a.g ? t + (x[e] + y[e]) : t + y[e];
         }
-      } else {
-        add_row_w<bf16, NR>(v, g2p, h);
       }
       store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
     }
+    if (rd + rw.step < rw.end) tile_ids(rd + rw.step, sid_next, did_next);
     EB_STAMP(11);
 #ifdef AGN_EB_STAMPS
     ++ntile_done;
@@ -531,7 +569,11 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
 #pragma unroll
       for (int y = 0; y < 2; ++y) dw[l][x][y] = f32x16{};
     }
-  int n = 0;
+  int n = 0, pre0 = 0, pre1 = 0;
+  // the dW waves outrank their SIMD's chain wave: their four MFMAs per item issue between the
+  // chain's instead of queueing behind a whole 32-MFMA chain step (which holds the ring slot
+  // the other chain waves are waiting for)
+  __builtin_amdgcn_s_setprio(2);
 #ifdef AGN_EB_STAMPS
   unsigned long long waited = 0;
   const unsigned long long tstart = __builtin_amdgcn_s_memtime();
@@ -539,33 +581,59 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   for (int rd = rw.first; rd < rw.end; rd += rw.step) {
     const int cmax = min(CW, ntiles - rd * CW);
 #pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int li = s >> 1;  // 0: L = 3, 1: L = 2, 2: L = 1
-      for (int cc = 0; cc < cmax; ++cc, ++n) {
-        const int k = n % NSLOT, j = n / NSLOT;
+    for (int li = 0; li < 3; ++li) {  // 0: L = 3, 1: L = 2, 2: L = 1
+      for (int cc = 0; cc < cmax; ++cc, n += 2) {
+        // a chain wave's pair (items n, n + 1: both halves of its tile) is taken at once: one
+        // LDS round trip for its 16 reads instead of two
+        const int k0 = n % NSLOT, j0 = n / NSLOT;
+        const int k1 = (n + 1) % NSLOT, j1 = (n + 1) / NSLOT;
 #ifdef AGN_EB_STAMPS
         const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-        wait_ge(&filled[k], j + 1);
-        waited += __builtin_amdgcn_s_memtime() - t0;
-#else
-        wait_ge(&filled[k], j + 1);
 #endif
-        const char* sb = lds + OFF_RING + k * SLOT_B;
-        const bf16x8 g0 = tr_pair(sb + 512 * ob + t1, sb + 512 * ob + t2);
-        const bf16x8 g1 = tr_pair(sb + 512 * (ob + 1) + t1, sb + 512 * (ob + 1) + t2);
-        const bf16x8 x0 = tr_pair(sb + HALF_B + 512 * ib + t1, sb + HALF_B + 512 * ib + t2);
-        const bf16x8 x1 = tr_pair(sb + HALF_B + 512 * (ib + 1) + t1, sb + HALF_B + 512 * (ib + 1) + t2);
-        lgkm_drain();
-        if (lane == 0) __hip_atomic_fetch_add(&consumed[k], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        mfma(dw[li][0][0], g0, x0);
-        mfma(dw[li][0][1], g0, x1);
-        mfma(dw[li][1][0], g1, x0);
-        mfma(dw[li][1][1], g1, x1);
-        if ((d & 1) == 0) {
+        if (pre0 < j0 + 1) wait_ge(&filled[k0], j0 + 1);
+        if (pre1 < j1 + 1) wait_ge(&filled[k1], j1 + 1);
+#ifdef AGN_EB_STAMPS
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+        waited += t1 - t0;
+        unsigned long long* ist = (a.stamps && blockIdx.x == 0 && n >= 24 && n < 72)
+                                      ? a.stamps + 2048 + (d * 48 + n - 24) * 3 : nullptr;
+        if (ist && lane == 0) {
+          ist[0] = ist[3] = t0;
+          ist[1] = ist[4] = t1;
+        }
+#endif
+        bf16x8 gf[2][2], xf[2][2];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            dbs[li][0] += (float)g0[e];
-            dbs[li][1] += (float)g1[e];
+        for (int q2 = 0; q2 < 2; ++q2) {
+          const char* sb = lds + OFF_RING + (q2 ? k1 : k0) * SLOT_B;
+          gf[q2][0] = tr_pair(sb + 512 * ob + t1, sb + 512 * ob + t2);
+          gf[q2][1] = tr_pair(sb + 512 * (ob + 1) + t1, sb + 512 * (ob + 1) + t2);
+          xf[q2][0] = tr_pair(sb + HALF_B + 512 * ib + t1, sb + HALF_B + 512 * ib + t2);
+          xf[q2][1] = tr_pair(sb + HALF_B + 512 * (ib + 1) + t1, sb + HALF_B + 512 * (ib + 1) + t2);
+        }
+        lgkm_drain();
+        if (lane == 0) {
+          __hip_atomic_fetch_add(&consumed[k0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&consumed[k1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+#ifdef AGN_EB_STAMPS
+        if (ist && lane == 0) ist[2] = ist[5] = __builtin_amdgcn_s_memtime();
+#endif
+        // the next pair's flags are read now, their latency under this pair's MFMAs
+        pre0 = __hip_atomic_load(&filled[(n + 2) % NSLOT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pre1 = __hip_atomic_load(&filled[(n + 3) % NSLOT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int q2 = 0; q2 < 2; ++q2) {
+          mfma(dw[li][0][0], gf[q2][0], xf[q2][0]);
+          mfma(dw[li][0][1], gf[q2][0], xf[q2][1]);
+          mfma(dw[li][1][0], gf[q2][1], xf[q2][0]);
+          mfma(dw[li][1][1], gf[q2][1], xf[q2][1]);
+          if ((d & 1) == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              dbs[li][0] += (float)gf[q2][0][e];
+              dbs[li][1] += (float)gf[q2][1][e];
+            }
           }
         }
       }

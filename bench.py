@@ -142,6 +142,35 @@ def cpu_info():
     return name
 
 
+def host_threads():
+    """Every core this process may run on: its CPU affinity set, bounded by a cgroup v2 CPU quota
+    when one is set (a quota of Q CPUs makes more than Q threads slower, not faster)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
+def latest_profile(suffix):
+    """The newest committed profiles/r<round>[e]_<suffix> (round names sort: r2_ < r2e_ < r3_)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + suffix)))
+    return fs[-1] if fs else None
+
+
+def latest_cpu_plan():
+    """The newest committed profiles/r*_cpu_plan.json (bench.py --cpu-plan on the GPU box)."""
+    f = latest_profile("cpu_plan.json")
+    if not f:
+        return None, None
+    return os.path.basename(f), json.load(open(f))
+
+
 def _median_time(fn, reps=3, label=None):
     """1 warm-up + median of `reps`; with a label, a progress line per run and a heartbeat every
     60 s on stderr (a multi-minute CPU row must not look hung to a job watchdog)."""
@@ -175,7 +204,7 @@ def cpu_baseline(num_scales, nu=250, nv=200):
     same BSMS model's forward on a 50,000-node / 299,000-edge ellipsoid (~20 s of CPU work)."""
     from aerognn.meshgen import ellipsoid
     from oracle import refcpu as R
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads, tinfo = host_threads()
     torch.set_num_threads(nthreads)
     m = ellipsoid(nu, nv, seed=0)
     t = {k: torch.from_numpy(v) for k, v in m.items()}
@@ -196,12 +225,21 @@ def cpu_baseline(num_scales, nu=250, nv=200):
         with torch.no_grad():
             R.bsms_forward(p, t["x"], t["edge_attr"], t["edge_index"], cfg, batch, t["pos"], stable=True)
     dt = _median_time(fwd)
-    return {"value": eu / dt / 1e6, "unit": "M edge-updates/s", "cores": nthreads, "kind": "port",
-            "cpu": cpu_info(), "torch": torch.__version__, "dtype": "f32",
-            "sample": f"fp32 forward (no_grad) of the same BSMS-{num_scales} model, oracle/refcpu.py, on a "
-                      f"{nu * nv}-node/{m['edge_index'].shape[1]}-edge ellipsoid ({eu} EU); 1 warm-up, median of 3 "
-                      f"= {dt:.2f} s; torch threads={nthreads}. Full BASELINE.md §3 plan (C1-C3 fwd, C1/C2 train): "
-                      f"bench.py --cpu-plan, committed as profiles/r2_cpu_plan.json"}
+    out = {"value": eu / dt / 1e6, "unit": "M edge-updates/s", "cores": nthreads, "threads": tinfo, "kind": "port",
+           "cpu": cpu_info(), "torch": torch.__version__, "dtype": "f32",
+           "sample": f"fp32 forward (no_grad) of the same BSMS-{num_scales} model, oracle/refcpu.py, on a "
+                     f"{nu * nv}-node/{m['edge_index'].shape[1]}-edge ellipsoid ({eu} EU); 1 warm-up, median of 3 "
+                     f"= {dt:.2f} s; torch threads={nthreads} (every CPU of the affinity set, bounded by the cgroup "
+                     f"quota). The full-size C3 forward (minutes of CPU work) is c3_forward, from bench.py --cpu-plan"}
+    name, plan = latest_cpu_plan()
+    if plan:
+        row = next((r for r in plan["rows"] if r["config"] == "C3" and r["mode"] == "fwd"), None)
+        if row:
+            out["c3_forward"] = {"value": row["M_EU_per_s"], "unit": "M edge-updates/s", "seconds": row["seconds"],
+                                 "cores": plan["cores"], "nodes": row["nodes"], "edges": row["edges"],
+                                 "source": f"profiles/{name} (bench.py --cpu-plan on this box type, "
+                                           f"{plan['protocol']})"}
+    return out
 
 
 def cpu_plan():
@@ -209,9 +247,9 @@ def cpu_plan():
     of 3, fp32, oracle/refcpu.py on host cores (minutes of CPU work; run once, results committed)."""
     from aerognn.meshgen import ellipsoid
     from oracle import refcpu as R
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads, tinfo = host_threads()
     torch.set_num_threads(nthreads)
-    out = {"cpu": cpu_info(), "cores": nthreads, "torch": torch.__version__, "dtype": "f32",
+    out = {"cpu": cpu_info(), "cores": nthreads, "threads": tinfo, "torch": torch.__version__, "dtype": "f32",
            "protocol": "1 warm-up, median of 3", "rows": []}
     for name, (nu, nv), S, modes in (("C1", (40, 25), 1, ("fwd", "train")), ("C2", (400, 250), 1, ("fwd", "train")),
                                      ("C3", (1000, 1000), 4, ("fwd",))):
@@ -291,8 +329,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the secondary C4 strong-scaling measurement")
     ap.add_argument("--cpu-plan", action="store_true", help="run BASELINE.md §3's full CPU plan and exit")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "r2e_pmc_traffic.json"),
-                    help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels")
+    ap.add_argument("--traffic", default=latest_profile("pmc_traffic.json"),
+                    help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels "
+                         "and per step (default: the newest profiles/r*_pmc_traffic.json)")
     args = ap.parse_args()
     if args.cpu_plan:
         print(json.dumps(cpu_plan()))
@@ -436,32 +475,45 @@ def main():
                               "flops, + pool/unpool/encoders/decoder; x3 for training"}
     else:
         step_roof = None
+    pmc = None
+    if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and args.mode == "train" \
+            and args.model == "bsms_mgn":
+        pmc = json.load(open(args.traffic))
+    if step_roof is not None and pmc and pmc.get("per_step_bytes"):
+        step_roof["traffic_bytes"] = pmc["per_step_bytes"]
+        step_roof["traffic_over_alg8d"] = pmc["per_step_bytes"] / step_roof["alg_bytes"]
+        step_roof["traffic_source"] = os.path.relpath(args.traffic, ROOT) + " (PMC FETCH_SIZE/WRITE_SIZE passes)"
     if kernels:
-        tag, kt = next(iter(kernels.items()))  # most device time over ALL recorded launches
-        n, ms, by, fl, impl, has = kt["_sum"]
-        traffic = None
-        if args.traffic and os.path.exists(args.traffic) and args.config == "c3" and args.mode == "train" \
-                and args.model == "bsms_mgn":
-            traffic = json.load(open(args.traffic)).get("per_launch_bytes", {}).get(tag)
-        # §8(d) share when the kernel has one; a kernel outside the fused minimum (wgrad: its G / X
-        # reads are re-reads a fused backward avoids) is priced on its operator I/O, labelled so
-        basis_bytes = (by if by else impl) if has else None
-        ach = basis_bytes / n / (ms / n * 1e-3) / 1e9 if basis_bytes else None
-        roof = {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": traffic,
-                "alg_bytes_per_launch": basis_bytes / n if basis_bytes else None,
-                "traffic_over_alg": (traffic / (basis_bytes / n)) if (traffic and basis_bytes) else None,
-                "avg_launch_us": 1e3 * ms / n, "launches_per_step": n / args.profile_steps,
-                "mfma_tflops": round(fl / (ms * 1e-3) / 1e12, 2) if has else None, "mfma_peak": MFMA_PEAK[dname],
-                "alg8d_bytes_per_launch": by / n if has else None,
-                "alg_basis": ("SURVEY §8(d) share of the fused layer (DESIGN.md §5)" if (has and by) else
-                              "operator I/O (G and X read once, dW/db written): this kernel's §8(d) fused share "
-                              "is 0 bytes, all of its traffic is re-reads of saved training state" if has else
-                              "none: untagged kernel"),
-                "step": step_roof}
+        def kroof(tag, basis_bytes, basis):
+            n, ms, by, fl, impl, has = kernels[tag]["_sum"]
+            ach = basis_bytes / (ms * 1e-3) / 1e9
+            traffic = (pmc or {}).get("per_launch_bytes", {}).get(tag)
+            return {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "alg_bytes_per_launch": basis_bytes / n,
+                    "traffic_over_alg": (traffic / (basis_bytes / n)) if traffic else None,
+                    "avg_launch_us": 1e3 * ms / n, "launches_per_step": n / args.profile_steps,
+                    "share_of_step": kernels[tag]["share_of_step"],
+                    "mfma_tflops": round(fl / (ms * 1e-3) / 1e12, 2), "mfma_peak": MFMA_PEAK[dname],
+                    "alg_basis": basis}
+        # the headline roofline: the kernel with the most device time among those that HAVE a §8(d)
+        # share (wgrad has none: a fused backward never re-reads G and X)
+        k8 = [t for t, v in kernels.items() if v["_sum"][5] and v["_sum"][2] > 0]
+        if k8:
+            roof = kroof(k8[0], kernels[k8[0]]["_sum"][2], "SURVEY §8(d) share of the fused layer (DESIGN.md §5)")
+        top = next(iter(kernels))
+        if top != (k8[0] if k8 else None) and kernels[top]["_sum"][5]:
+            # the top kernel has no §8(d) share: its own operator I/O (G and X read once, dW/db
+            # written) prices it, in a separately named object
+            oio = kroof(top, kernels[top]["_sum"][4], "operator I/O (G and X read once, dW/db written); "
+                                                      "its §8(d) fused share is 0 bytes")
+            if roof is not None:
+                roof["top_kernel_operator_io"] = oio
+        if roof is not None:
+            roof["step"] = step_roof
         for v in kernels.values():
             v.pop("_sum")
-    elif step_roof:
+    if roof is None and step_roof:
         roof = {"kernel": None, "bound": step_roof["bound"], "achieved": step_roof["achieved_GBs"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_roof["frac"], "traffic": None, "step": step_roof}
 

@@ -58,11 +58,28 @@ def main():
         run()
     torch.cuda.synchronize()
     print(f"E = {E}: {1e3 * (time.perf_counter() - t) / 5:.3f} ms per launch (incl. the slab reduce)")
-    core.STAMPS = torch.zeros(2 * 8 * 8 * 16, dtype=torch.int64, device=dev)
+    core.STAMPS = torch.zeros(4096, dtype=torch.int64, device=dev)
     run()
     torch.cuda.synchronize()
-    st = core.STAMPS.cpu().numpy().reshape(2, 8, 8, 16).astype(np.int64)
+    allst = core.STAMPS.cpu().numpy().astype(np.int64)
+    st = allst[:2048].reshape(2, 8, 8, 16)
     core.STAMPS = None
+    # item timeline of block 0, rounds 1 and 2 (items 24..71): produce enter / slot free / flagged,
+    # and per dW wave poll start / detect / released
+    dwi = allst[2048:2048 + 576].reshape(4, 48, 3)
+    chi = allst[2048 + 576:2048 + 576 + 144].reshape(4, 2, 6, 3)
+    t0 = chi[:, 0, 0, 0].min()
+    print("items  chain  enter  slotfree  flagged | dW detect (d0..d3, both items) | dW released | slot-wait  write  detect  read")
+    for r in (1, 2):
+        for li in range(3):
+            for c in range(4):
+                n = 24 * r + 8 * li + 2 * c
+                pe, pf, pg = chi[c, r - 1, 2 * li] - t0
+                det = dwi[:, n - 24:n - 22, 1] - t0
+                rel = dwi[:, n - 24:n - 22, 2] - t0
+                print(f"{n:3d},{n + 1:3d} c{c} L{3 - li} {pe:7d} {pf:7d} {pg:7d} | " + " ".join(f"{x:7d}" for x in det.max(1)) +
+                      " | " + " ".join(f"{x:7d}" for x in rel.max(1)) +
+                      f" | {pf - pe:6d} {pg - pf:6d} {det[:, 0].max() - pg:6d} {rel[:, 1].max() - det[:, 0].max():6d}")
     for sel in range(2):
         print(f"block {0 if sel == 0 else 128}:")
         tot = np.zeros(len(PHASES))

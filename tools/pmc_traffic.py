@@ -1,12 +1,15 @@
 """Per-launch HBM traffic of the hot kernels from two rocprofv3 PMC passes.
 
-Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON
+Usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [STEPS]
 
 FETCH_DIR / WRITE_DIR hold the `--pmc FETCH_SIZE` and `--pmc WRITE_SIZE` passes
 (`--output-format csv`, separate runs: the two counters do not fit one TCC pass on gfx950).
 Correction applied as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KiB) reports half the
 bytes of a wide 16-B/lane coalesced read on gfx950 -> x2; WRITE_SIZE (KiB) is exact for
-16-B/lane stores.  Result: bytes per launch, averaged over every launch of the kernel.
+16-B/lane stores.  Result: bytes per launch, averaged over every launch of the kernel, and with
+STEPS (the train steps the profiled bench.py ran: warmup + timed + instrumented) the bytes per step
+of every kernel the run launched (one-time setup launches included: host->device copies and
+parameter init, well under 1 % of a step).
 """
 import csv
 import glob
@@ -43,6 +46,7 @@ def _per_kernel(rows, counter):
 
 def main():
     fdir, wdir, out = sys.argv[1:4]
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else None
     fetch = _per_kernel(_rows(fdir), "FETCH_SIZE")
     write = _per_kernel(_rows(wdir), "WRITE_SIZE")
     kern = {}
@@ -59,7 +63,9 @@ def main():
         if hit:
             n = sum(h["launches"] for h in hit)
             tags[tag] = sum(h["bytes"] * h["launches"] for h in hit) / n
-    json.dump({"per_launch_bytes": tags, "kernels": kern,
+    total = sum(v["bytes"] * v["launches"] for v in kern.values())
+    json.dump({"per_launch_bytes": tags, "kernels": kern, "total_bytes": total, "steps": steps,
+               "per_step_bytes": total / steps if steps else None,
                "correction": "FETCH_SIZE*2*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM)"},
               open(out, "w"), indent=1)
     print(json.dumps(tags))

@@ -19,7 +19,8 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/p
     python $B --steps 1 --warmup 1 > gpurun_out/pmc_fetch_$TAG.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$TAG -o c3 -- \
     python $B --steps 1 --warmup 1 > gpurun_out/pmc_write_$TAG.log 2>&1
-python tools/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_traffic_$TAG.json
+# 3 steps per PMC run: 1 warm-up, 1 timed, 1 instrumented (bench.py --profile-steps 1)
+python tools/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_traffic_$TAG.json 3
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d gpurun_out/pmc_mfma_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_mfma_$TAG.log 2>&1
 python tools/mfma_busy.py gpurun_out/pmc_mfma_$TAG gpurun_out/mfma_$TAG.json
