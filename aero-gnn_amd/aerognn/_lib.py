@@ -59,7 +59,7 @@ MAX_WGRAD = 8
 class WgradDesc(C.Structure):
     _fields_ = [("g", vp), ("x", vp), ("ldg", i32), ("ldx", i32), ("m", i32), ("k", i32), ("rows", i32),
                 ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp),
-                ("g_tiled", i32), ("x_tiled", i32), ("nsplit", i32), ("_pad", i32)]
+                ("g_tiled", i32), ("x_tiled", i32), ("nsplit", i32), ("_pad", i32), ("xidx", vp)]
 
 
 class WgradBatch(C.Structure):
@@ -94,7 +94,7 @@ _lib = None
 # to) and recorded under its name, unless an enclosing core.timed(...) already times it under a
 # finer tag (edge_fwd, node_bwd, ...). Nothing is recorded when PROF is None.
 LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_partials", "agn_wgrad", "agn_colsum",
-            "agn_segment_sum", "agn_gather_rows", "agn_radix_sort_u64", "agn_row_ptr", "agn_row_ptr_i64",
+            "agn_segment_sum", "agn_segment_sum2", "agn_gather_rows", "agn_radix_sort_u64", "agn_row_ptr", "agn_row_ptr_i64",
             "agn_exclusive_scan_i32", "agn_pool_sort_keys", "agn_pool_assign", "agn_pool_edge_candidates",
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
@@ -163,6 +163,7 @@ def lib():
             "agn_wgrad_plan": (i32, [C.POINTER(WgradBatch)]),
             "agn_colsum": (i32, [vp, i32, i32, vp, i32, vp, vp]),
             "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
+            "agn_segment_sum2": (i32, [i32, i32, i32, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp]),
             "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
             "agn_segment_max": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, vp]),
             "agn_segment_max_backward": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),

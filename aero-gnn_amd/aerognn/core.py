@@ -334,6 +334,16 @@ def segment_sum(rows, k, ptr_t, perm, src, out, mean=False, src_ld=None, out_ld=
     return out
 
 
+def segment_sum2(rows, k, base, a, b, out):
+    """out = base + segment sums of a = (ptr, perm, src) + of b, fp32 in that order (out may be
+    base; base None = 0)."""
+    (pa, qa, sa), (pb, qb, sb) = a, b
+    check(L.lib().agn_segment_sum2(rows, k, dt_code(sa.dtype), ptr(base), base.stride(0) if base is not None else 0, ptr(pa), ptr(qa), ptr(sa),
+                                   sa.stride(0), ptr(pb), ptr(qb), ptr(sb), sb.stride(0), ptr(out), out.stride(0),
+                                   stream()), "segment_sum2")
+    return out
+
+
 def segment_max(rows, k, ptr_t, perm, src, out, argmax):
     check(L.lib().agn_segment_max(rows, k, dt_code(src.dtype), ptr(ptr_t), ptr(perm), ptr(src), src.stride(0), ptr(out),
                                   out.stride(0), ptr(argmax), stream()), "segment_max")
@@ -378,10 +388,12 @@ class WGrad:
     def __init__(self):
         self.items = []
 
-    def add(self, G, X, dw, db=None):
-        assert G.dtype == X.dtype and logical_rows(G) == logical_rows(X)
+    def add(self, G, X, dw, db=None, xidx=None):
+        """xidx: X is gathered, row r of the operand = X[xidx[r]] (int32, one entry per row of G)."""
+        assert G.dtype == X.dtype and logical_rows(G) == (logical_rows(X) if xidx is None else xidx.numel())
         assert dw.dtype == torch.float32 and dw.stride(1) == 1
-        self.items.append((G, X, dw, db))
+        assert xidx is None or (xidx.dtype == torch.int32 and not is_tiled(X))
+        self.items.append((G, X, dw, db, xidx))
 
     def run(self):
         lib = L.lib()
@@ -389,28 +401,29 @@ class WGrad:
             chunk = self.items[i:i + L.MAX_WGRAD]
             dev = chunk[0][0].device
             live = []
-            for G, X, dw, db in chunk:
+            for G, X, dw, db, xi in chunk:
                 if logical_rows(G) == 0:
                     dw.zero_()
                     if db is not None:
                         db.zero_()
                 else:
-                    live.append((G, X, dw, db))
+                    live.append((G, X, dw, db, xi))
             if not live:
                 continue
             b = L.WgradBatch()
             b.n = len(live)
-            for j, (G, X, dw, db) in enumerate(live):
+            for j, (G, X, dw, db, xi) in enumerate(live):
                 b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], logical_rows(G),
-                                     dw.stride(0), None, None, ptr(dw), ptr(db), int(is_tiled(G)), int(is_tiled(X)), 0, 0)
+                                     dw.stride(0), None, None, ptr(dw), ptr(db), int(is_tiled(G)), int(is_tiled(X)), 0, 0,
+                                     ptr(xi))
             check(lib.agn_wgrad_plan(C.byref(b)), "wgrad_plan")  # one uniform split count, from the largest desc
             sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], b.d[j].nsplit))
-                     for j, (G, X, _, _) in enumerate(live)]
+                     for j, (G, X, _, _, _) in enumerate(live)]
             bsz = [b.d[j].nsplit * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0
-                   for j, (G, _, _, db) in enumerate(live)]
+                   for j, (G, _, _, db, _) in enumerate(live)]
             scratch = torch.empty(sum(sizes) + sum(bsz), dtype=torch.float32, device=dev)
             o = 0
-            for j, (G, X, dw, db) in enumerate(live):
+            for j, (G, X, dw, db, _) in enumerate(live):
                 b.d[j].dw_partial = ptr(scratch[o:o + sizes[j]])
                 o += sizes[j]
                 if db is not None:
@@ -420,8 +433,8 @@ class WGrad:
             # share is 0 (a fused backward keeps G in registers), so the alg_bytes slot carries 0
             s_el = live[0][0].element_size()
             io = sum(logical_rows(G) * (G.shape[1] + X.shape[1]) * s_el + 4 * G.shape[1] * (X.shape[1] + 1)
-                     for G, X, _, _ in live)
-            fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _ in live)
+                     for G, X, _, _, _ in live)
+            fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _, _ in live)
             with timed("wgrad", (0.0, fl, io)):
                 check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
         self.items = []

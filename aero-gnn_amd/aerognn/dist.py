@@ -15,13 +15,17 @@ import torch
 import torch.distributed as dist
 
 
-def init_from_env(backend=None):
+def init_from_env(backend=None, force=None):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/MASTER_*).
 
     Backend: `backend`, else $AEROGNN_DIST_BACKEND, else "nccl" (= RCCL on ROCm) when a GPU is
     present and "gloo" otherwise. gloo with device tensors stages through host memory
-    (rehearsing N ranks on one GPU; never the production path)."""
-    if not dist.is_available() or int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+    (rehearsing N ranks on one GPU; never the production path). A single process stays
+    undistributed unless `force` (or $AEROGNN_DIST_FORCE=1): then a world of one runs the whole
+    collective path (bucketed async all-reduce, wait, unpack) on a real communicator."""
+    if force is None:
+        force = os.environ.get("AEROGNN_DIST_FORCE", "0") == "1"
+    if not dist.is_available() or (int(os.environ.get("WORLD_SIZE", "1")) <= 1 and not force):
         return 0, 1
     if not dist.is_initialized():
         if backend is None:
@@ -50,9 +54,14 @@ def world():
     return 0, 1
 
 
+def active() -> bool:
+    """A process group exists (also a forced world of one): collectives run."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def global_count(n_local: int, device) -> float:
     t = torch.tensor([float(n_local)], dtype=torch.float64, device=device)
-    if world()[1] > 1:
+    if active():
         all_reduce_(t)
     return float(t.item())
 
@@ -100,7 +109,8 @@ class GradAllReduce:
         self._works = {}
         self._pending = None
         self._hooks = []
-        if world()[1] > 1:
+        self.launched_in_hooks = 0  # buckets the last armed backward launched from its hooks
+        if active():
             where = {}
             for bi, b in enumerate(self.buckets):
                 for p in b:
@@ -116,10 +126,11 @@ class GradAllReduce:
                           for b in self.buckets]
 
     def arm(self):
-        if world()[1] <= 1:
+        if not active():
             return
         self._armed = True
         self._works = {}
+        self.launched_in_hooks = 0
         self._pending = [len(b) for b in self.buckets]
         self._next = 0
 
@@ -133,6 +144,7 @@ class GradAllReduce:
             while self._next < len(self.buckets) and self._pending[self._next] == 0:
                 self._launch(self._next)
                 self._next += 1
+                self.launched_in_hooks += 1
         return fire
 
     def _launch(self, bi):
@@ -149,8 +161,7 @@ class GradAllReduce:
         self._works[bi] = all_reduce_(flat, async_op=True)
 
     def __call__(self):
-        rank, ws = world()
-        if ws <= 1:
+        if not active():
             return
         for bi in range(len(self.buckets)):  # the rest, in index order
             if bi not in self._works:

@@ -26,7 +26,7 @@ from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
-                   scatter_rows, segment_max, segment_max_backward, segment_sum, stream)
+                   scatter_rows, segment_max, segment_max_backward, segment_sum, segment_sum2, stream)
 
 
 def _c(t):
@@ -144,9 +144,11 @@ def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk, wg=None):
         dw = torch.empty(M, K, dtype=torch.float32, device=dev)
         db = torch.empty(M, dtype=torch.float32, device=dev) if b is not None else None
         if l == 0 and isinstance(inputs0, (list, tuple)):
+            # column blocks of dW; an (X, idx) block is the gathered operand X[idx] (agn_wgrad's xidx)
             k0 = 0
             for j, X in enumerate(inputs0):
-                wg.add(G, X, dw[:, k0:k0 + X.shape[1]], db if j == 0 else None)
+                X, xi = X if isinstance(X, tuple) else (X, None)
+                wg.add(G, X, dw[:, k0:k0 + X.shape[1]], db if j == 0 else None, xidx=xi)
                 k0 += X.shape[1]
         else:
             wg.add(G, inputs0 if l == 0 else acts[l - 1], dw, db)
@@ -230,7 +232,7 @@ class MLPFn(torch.autograd.Function):
                 dxs = torch.empty(x.shape[0], x.shape[1], dtype=dt, device=x.device)
                 segment_sum(x.shape[0], x.shape[1], rp, perm, dx, dxs)
                 dx = dxs
-        x0 = x if ctx.idx is None else x.index_select(0, ctx.idx.long())
+        x0 = x if ctx.idx is None else [(x, ctx.idx)]  # the gathered rows, read through agn_wgrad's xidx
         grads = _chain_param_grads(spec, gpre, x0, ctx.acts, part, nblk)
         return (dx, None, None, None, *grads)
 
@@ -494,11 +496,10 @@ class GMPFn(torch.autograd.Function):
             grads_edge = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
             return (dx, de, None, None, None, *grads_edge, *grads_node)
         else:
-            ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
-            dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))
-            dx = dx + ds + dd
-            xs = x.index_select(0, lv.src.long())
-            xd = x.index_select(0, lv.dst.long())
+            # concat edge MLP: dx += scatter_add(d x_src, src) + scatter_add(d x_dst, dst) in one pass
+            # (fp32, one rounding), and W_0's x_src / x_dst column blocks from gathered operands
+            segment_sum2(N, H, dx, (lv.rowptr_src, lv.perm_src, dxs), (lv.rowptr, None, dxd), dx)
+            xs, xd = (x, lv.src), (x, lv.dst)
             grads_edge = _chain_param_grads(es, gpre_e, [xs, xd, e] if spec.gmp_order else [e, xs, xd],
                                             ea, part_e, nb_e)
         grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n)
@@ -685,12 +686,9 @@ class EdgeBlockFn(torch.autograd.Function):
             wg.run()
             grads = [eg[0], dws.to(eb.src_lin.dtype), dwd.to(eb.dst_lin.dtype), dbd.to(eb.bias.dtype)] + eg[1:]
         else:
-            ds = segment_sum(N, H, lv.rowptr_src, lv.perm_src, dxs, torch.empty(N, H, dtype=dt, device=dev))
-            dd = segment_sum(N, H, lv.rowptr, None, dxd, torch.empty(N, H, dtype=dt, device=dev))
-            dx = ds + dd
-            xs = x.index_select(0, lv.src.long())
-            xd = x.index_select(0, lv.dst.long())
-            grads = _chain_param_grads(es, gpre, [e, xs, xd], ea, part, nb)
+            dx = segment_sum2(N, H, None, (lv.rowptr_src, lv.perm_src, dxs), (lv.rowptr, None, dxd),
+                              torch.empty(N, H, dtype=dt, device=dev))
+            grads = _chain_param_grads(es, gpre, [e, (x, lv.src), (x, lv.dst)], ea, part, nb)
         return (dx, de, None, None, None, *grads)
 
 

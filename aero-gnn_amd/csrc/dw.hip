@@ -50,7 +50,9 @@ struct StageRegs {
     row = t * 32 + (rem & 31);
     hh = (rem >> 5) & 1;
   }
-  AGN_DEV void load(const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0, int tiled) {
+  // idx (row-major operands only): logical row r is g's row idx[r] (a gathered operand)
+  AGN_DEV void load(const T* __restrict__ g, int ld, int rows, int cols, int r0, int c0, int tiled,
+                    const int32_t* __restrict__ idx = nullptr) {
     if (tiled) {
       const uint4* gu = reinterpret_cast<const uint4*>(g) + (size_t)(r0 >> 5) * (CHUNKS / 2) * 64;
       if (r0 + DW_ROWS <= rows) {
@@ -73,7 +75,8 @@ struct StageRegs {
       for (int j = 0; j < NCH; ++j) {
         const int i = threadIdx.x + j * DW_THREADS;
         const int r = i / CHUNKS, ch = i - r * CHUNKS;
-        v[j] = *reinterpret_cast<const uint4*>(g + (size_t)(r0 + r) * ld + c0 + ch * PER16);
+        const size_t gr = idx ? (size_t)idx[r0 + r] : (size_t)(r0 + r);
+        v[j] = *reinterpret_cast<const uint4*>(g + gr * ld + c0 + ch * PER16);
       }
     } else {
 #pragma unroll
@@ -81,11 +84,12 @@ struct StageRegs {
         const int i = threadIdx.x + j * DW_THREADS;
         const int r = i / CHUNKS, ch = i - r * CHUNKS;
         const int gr = r0 + r;
+        const size_t sr = (gr < rows && idx) ? (size_t)idx[gr] : (size_t)gr;
         T e8[PER16];
 #pragma unroll
         for (int e = 0; e < PER16; ++e) {
           const int gc = c0 + ch * PER16 + e;
-          e8[e] = (gr < rows && gc < cols) ? g[(size_t)gr * ld + gc] : from_f<T>(0.f);
+          e8[e] = (gr < rows && gc < cols) ? g[sr * ld + gc] : from_f<T>(0.f);
         }
         v[j] = *reinterpret_cast<const uint4*>(e8);
       }
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   StageRegs<T> rg, rx;
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
-    rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled);
+    rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled, d.xidx);
   }
   for (int r0 = rbeg; r0 < rend; r0 += DW_ROWS) {
     __syncthreads();
@@ -175,7 +179,7 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     __syncthreads();
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
-      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled);
+      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, d.xidx);
     }
     if (d.db_partial && kb == 0) {
       const int col = threadIdx.x & (DW_BLK - 1), q = threadIdx.x >> 7;
@@ -389,6 +393,7 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
     agn_wgrad_desc& d = bb.d[i];
     if (d.m < 1 || d.k < 1 || d.rows < 0) return AGN_E_ARG;
     if ((d.g_tiled && d.m != DW_BLK) || (d.x_tiled && d.k != DW_BLK)) return AGN_E_SHAPE;
+    if (d.xidx && d.x_tiled) return AGN_E_ARG;
     if (nsplit > 0) d.nsplit = nsplit;
     if (d.nsplit < 1) return AGN_E_ARG;
     total += out_blocks(d) * d.nsplit;

@@ -95,6 +95,53 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   }
 }
 
+// out[r] = base[r] + (group a of r) + (group b of r): the concat edge MLP's node gradient in one
+// pass (agn_segment_sum2). Same thread layout and in-order fp32 accumulation as segment_sum_kernel.
+template <typename T>
+AGN_DEV void seg_accum(float (&s)[8], int beg, int end, const int32_t* __restrict__ perm, const T* __restrict__ src,
+                       int ld, int f0, int k, bool vec) {
+  int j = beg;
+  for (; j + 1 < end; j += 2) {
+    const int e0 = perm ? perm[j] : j, e1 = perm ? perm[j + 1] : j + 1;
+    float x[8], y[8];
+    load8(x, src + (size_t)e0 * ld, f0, k, vec);
+    load8(y, src + (size_t)e1 * ld, f0, k, vec);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
+  }
+  if (j < end) {
+    const int e0 = perm ? perm[j] : j;
+    float x[8];
+    load8(x, src + (size_t)e0 * ld, f0, k, vec);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += x[i];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sum2_kernel(int rows, int k, const T* base, int base_ld,
+                                                           const int32_t* __restrict__ ptr_a,
+                                                           const int32_t* __restrict__ perm_a,
+                                                           const T* __restrict__ src_a, int lda,
+                                                           const int32_t* __restrict__ ptr_b,
+                                                           const int32_t* __restrict__ perm_b,
+                                                           const T* __restrict__ src_b, int ldb, T* out, int out_ld) {
+  const int sub = threadIdx.x & (SEG_TPR - 1);
+  const int r = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
+  if (r >= rows) return;
+  constexpr int A = 16 / sizeof(T);
+  const bool vec = ((k % A) == 0) && (!base || (base_ld % A) == 0) && ((lda % A) == 0) && ((ldb % A) == 0) &&
+                   ((out_ld % A) == 0) &&
+                   ((((uintptr_t)base) | ((uintptr_t)src_a) | ((uintptr_t)src_b) | ((uintptr_t)out)) & 15) == 0;
+  for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (base) load8(s, base + (size_t)r * base_ld, f0, k, vec);  // read before this thread's own store (out may alias)
+    seg_accum(s, ptr_a[r], ptr_a[r + 1], perm_a, src_a, lda, f0, k, vec);
+    seg_accum(s, ptr_b[r], ptr_b[r + 1], perm_b, src_b, ldb, f0, k, vec);
+    store8(out + (size_t)r * out_ld, f0, k, vec, s);
+  }
+}
+
 // Global max pooling (torch_geometric global_max_pool = scatter 'max' over graph ids, poolmgn.py:40):
 // out[r][f] = max over the members j of group r of src[perm[j]][f] (0 for an empty group, as the
 // zero-initialised scatter_reduce(include_self=False) leaves it), argmax[r][f] = the FIRST member
@@ -573,6 +620,16 @@ int seg_sum_t(int rows, int k, const int32_t* ptr, const int32_t* perm, const vo
 }
 
 template <typename T>
+int seg_sum2_t(int rows, int k, const void* base, int base_ld, const int32_t* ptr_a, const int32_t* perm_a,
+               const void* src_a, int lda, const int32_t* ptr_b, const int32_t* perm_b, const void* src_b, int ldb,
+               void* out, int out_ld, hipStream_t st) {
+  hipLaunchKernelGGL(segment_sum2_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, (const T*)base,
+                     base_ld, ptr_a, perm_a, (const T*)src_a, lda, ptr_b, perm_b, (const T*)src_b, ldb, (T*)out,
+                     out_ld);
+  return launch_status();
+}
+
+template <typename T>
 int gather_t(int rows, int k, const int32_t* idx, const void* src, int src_ld, const int32_t* cnt_ptr,
              const void* add, int add_ld, void* out, int out_ld, hipStream_t st) {
   hipLaunchKernelGGL(gather_rows_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, idx, (const T*)src,
@@ -594,6 +651,21 @@ int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_
   if (dtype == AGN_F32) return seg_sum_t<float>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_F16) return seg_sum_t<f16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
+  return AGN_E_DTYPE;
+}
+
+int agn_segment_sum2(int rows, int k, int dtype, const void* base, int base_ld, const int32_t* ptr_a,
+                     const int32_t* perm_a, const void* src_a, int lda, const int32_t* ptr_b, const int32_t* perm_b,
+                     const void* src_b, int ldb, void* out, int out_ld, void* stream) {
+  if (rows < 0 || k < 1) return AGN_E_ARG;
+  if (rows == 0) return 0;
+  if (!ptr_a || !src_a || !ptr_b || !src_b || !out) return AGN_E_ARG;
+  hipStream_t st = (hipStream_t)stream;
+#define AGN_SS2(T) seg_sum2_t<T>(rows, k, base, base_ld, ptr_a, perm_a, src_a, lda, ptr_b, perm_b, src_b, ldb, out, out_ld, st)
+  if (dtype == AGN_F32) return AGN_SS2(float);
+  if (dtype == AGN_BF16) return AGN_SS2(bf16);
+  if (dtype == AGN_F16) return AGN_SS2(f16);
+#undef AGN_SS2
   return AGN_E_DTYPE;
 }
 

@@ -390,6 +390,8 @@ def main():
                     f"edges per GPU, BFS hierarchy prebuilt")
         return model, [t], sum(Es), Es, workload, "weak", extra
 
+    allreduce_ref = []  # the headline step's GradAllReduce (for the line's collective record)
+
     def make_step(model, batches, extra):
         multi = extra.pop("multi", None)
 
@@ -399,6 +401,7 @@ def main():
             return model(b["x"], b["edge_attr"], b["edge_index"], multi_data=multi)
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
         allreduce = D.GradAllReduce(model.parameters())
+        allreduce_ref[:] = [allreduce]
         n_glob = D.global_count(sum(b["y"].numel() for b in batches), dev)
 
         def step():
@@ -538,6 +541,10 @@ def main():
         "roofline": roof,
         "kernels": kernels,
     }
+    if D.active():
+        out["collective"] = {"backend": torch.distributed.get_backend(), "world_size": ws,
+                             "buckets": len(allreduce_ref[0].buckets) if allreduce_ref else None,
+                             "launched_in_hooks": allreduce_ref[0].launched_in_hooks if allreduce_ref else None}
     if args.model == "bsms_mgn" and args.config == "c3" and args.mode == "train" and not args.no_c4:
         del model, batches, step
         torch.cuda.empty_cache()
@@ -560,7 +567,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if ws > 1:
+    if D.active():
         torch.distributed.destroy_process_group()
 
 

@@ -164,6 +164,9 @@ typedef struct {
   int g_tiled, x_tiled; /* operand in the AGN_TILED layout (then m resp. k == 128) */
   int nsplit;           /* row splits of this desc (agn_wgrad_plan); dw_partial holds nsplit slabs */
   int _pad;
+  const int32_t* xidx;  /* NULL, or a gathered X: logical row r is x's row xidx[r] (x[src] / x[dst]
+                           of the concat edge MLP, mgnLayer.py:10-49, without an [E][k] copy);
+                           row-major x only (x_tiled == 0) */
 } agn_wgrad_desc;
 typedef struct {
   int n;
@@ -202,6 +205,13 @@ int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* s
 /* out[r] = sum (or mean) of src[perm ? perm[j] : j] for j in ptr[r]..ptr[r+1]-1; [rows][k] */
 int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm,
                     const void* src, int src_ld, void* out, int out_ld, int mean, void* stream);
+/* out[r] = base[r] + sum_{j in ptr_a[r]..} src_a[perm_a ? perm_a[j] : j] + sum_{j in ptr_b[r]..}
+ * src_b[perm_b ? perm_b[j] : j], fp32 in that order, one rounding: the concat edge MLP's node
+ * gradient dx + scatter_add(d x_src, src) + scatter_add(d x_dst, dst) (mgnLayer.py:10-49 backward)
+ * in one pass. out may alias base; base NULL = 0. */
+int agn_segment_sum2(int rows, int k, int dtype, const void* base, int base_ld, const int32_t* ptr_a,
+                     const int32_t* perm_a, const void* src_a, int lda, const int32_t* ptr_b,
+                     const int32_t* perm_b, const void* src_b, int ldb, void* out, int out_ld, void* stream);
 /* Global max pooling (poolmgn.py:40, torch_geometric global_max_pool = scatter 'max'):
  * out[r][f] = max of src[perm ? perm[j] : j][f], j in ptr[r]..ptr[r+1]-1 (0 if empty), argmax[r][f]
  * = the first member row attaining it (-1 if empty); the backward writes dx[argmax[r][f]][f] =

@@ -48,10 +48,21 @@ def scatter_mean(src, index, dim=0, dim_size=None):
 # --------------------------------------------------------------------------------------
 
 
+# Test instrumentation: when set, PRE_ACT_TAP(prefix, index, h) sees every pre-activation the ReLU
+# MLPs below produce (tests/kinkfree.py conditions inputs away from ReLU kinks). No effect on values.
+PRE_ACT_TAP = None
+
+
+def _tap(pre, i, h):
+    if PRE_ACT_TAP is not None:
+        PRE_ACT_TAP(pre, i, h)
+    return h
+
+
 def mlp(p, pre, x, n_lin, ln=True, act=F.relu):
     for i in range(n_lin - 1):
         x = F.linear(x, p[f"{pre}.layers.{i}.weight"], p[f"{pre}.layers.{i}.bias"])
-        x = act(x)
+        x = act(_tap(pre, i, x))
     x = F.linear(x, p[f"{pre}.layers.{n_lin - 1}.weight"], p[f"{pre}.layers.{n_lin - 1}.bias"])
     if ln:
         w = p[f"{pre}.layer_norm.weight"]
@@ -70,10 +81,10 @@ def edge_block_sum(p, pre, e, x, ei, n_hid):
     mlp_dst_feat = F.linear(x, p[f"{pre}.dst_lin"], p[f"{pre}.bias"])
     src, dst = ei.long()
     h = mlp_edge_attr + mlp_src_feat[src] + mlp_dst_feat[dst]
-    h = F.relu(h)
+    h = F.relu(_tap(pre, 0, h))
     k = 1
     for _ in range(n_hid):
-        h = F.relu(F.linear(h, p[f"{pre}.mlp.{k}.weight"], p[f"{pre}.mlp.{k}.bias"]))
+        h = F.relu(_tap(pre, k, F.linear(h, p[f"{pre}.mlp.{k}.weight"], p[f"{pre}.mlp.{k}.bias"])))
         k += 2
     h = F.linear(h, p[f"{pre}.mlp.{k}.weight"], p[f"{pre}.mlp.{k}.bias"])
     w = p.get(f"{pre}.mlp.{k + 1}.weight")

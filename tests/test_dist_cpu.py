@@ -109,3 +109,36 @@ def test_single_rank_is_noop():
     D.GradAllReduce([p])()
     assert torch.equal(p.grad, torch.full((3,), 2.0))
     assert D.global_count(7, "cpu") == 7.0
+
+
+def _forced_one_worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      AEROGNN_DIST_FORCE="1")
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "aero-gnn_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    torch.set_num_threads(1)
+    from aerognn import dist as D
+    assert D.init_from_env(backend="gloo") == (0, 1) and D.active()
+    params = [torch.nn.Parameter(torch.randn(n, dtype=torch.float64)) for n in (5000, 3000, 7)]
+    loss = sum((p ** 2).sum() for p in params)
+    ar = D.GradAllReduce(params, bucket_bytes=16 << 10)
+    ar.arm()
+    loss.backward()
+    fired = ar.launched_in_hooks
+    ar()
+    ok = all(torch.equal(p.grad, 2 * p.detach()) for p in params)
+    torch.save({"fired": fired, "buckets": len(ar.buckets), "ok": ok}, out)
+    dist.destroy_process_group()
+
+
+def test_forced_world_of_one_runs_collective_path(tmp_path):
+    """AEROGNN_DIST_FORCE=1: a single process still builds a process group, and GradAllReduce's
+    armed path (hooks -> bucket pack -> async all-reduce -> wait -> unpack) runs and is an
+    identity (the GPU suite runs the same path on RCCL)."""
+    out = str(tmp_path / "f.pt")
+    mp.start_processes(_forced_one_worker, args=(_free_port(), out), nprocs=1, join=True, start_method="spawn")
+    r = torch.load(out, weights_only=True)
+    assert r["ok"] and r["buckets"] >= 2 and r["fired"] == r["buckets"], r

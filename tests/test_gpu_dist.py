@@ -5,6 +5,11 @@
    equal the single-process union-batch gradients of the same HIP model (fp32, summation-order
    tolerance).
 2. `bench.py --gpus 2` under torchrun prints one JSON line with n_gpus == 2.
+3. RCCL itself, once: a fresh torchrun child initialises the "nccl" backend (RCCL) before any GPU
+   call at world size 1 (AEROGNN_DIST_FORCE=1), and GradAllReduce's armed path (bucket packing
+   from the post-accumulate-grad hooks, async all-reduce on the RCCL communicator, wait, unpack)
+   leaves the gradients bitwise unchanged; bench.py on the same setup prints its JSON line with
+   the collective record.
 """
 import json
 import os
@@ -59,9 +64,10 @@ def _port():
     return p
 
 
-def _torchrun(script_args, timeout):
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", AEROGNN_DIST_BACKEND="gloo", AEROGNN_MEMLOG="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+def _torchrun(script_args, timeout, nproc=2, backend="gloo", **extra_env):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", AEROGNN_DIST_BACKEND=backend, AEROGNN_MEMLOG="0",
+               **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}"] + script_args
     return subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
 
@@ -100,3 +106,61 @@ def test_bench_two_ranks_json():
     d = json.loads(line)
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["scaling"] == "weak"
     assert d["config"]["parallelism"] == "dp2"
+
+
+RCCL_WORKER = r'''
+import os, sys, json
+sys.path[:0] = [{root!r}, os.path.join({root!r}, "aero-gnn_amd")]
+import numpy as np, torch
+os.environ["AEROGNN_MEMLOG"] = "0"
+from aerognn import dist as D
+rank, ws = D.init_from_env()  # the RCCL process group, before any GPU call of this process
+assert torch.distributed.get_backend() == "nccl" and ws == 1, (torch.distributed.get_backend(), ws)
+from aerognn.meshgen import ellipsoid
+from models.bsms_mgn import BiStridedMeshGraphNet
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+torch.manual_seed(0)
+model = BiStridedMeshGraphNet(6, 4, 4, **{kw!r}).to(dev)
+t = {{k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in ellipsoid(24, 16, seed=0).items()}}
+n_glob = D.global_count(t["y"].numel(), dev)  # itself an RCCL all-reduce
+def loss():
+    return D.mse_sum_loss(model(t["x"], t["edge_attr"], t["edge_index"], batch=None, pos=t["pos"]), t["y"], n_glob)
+loss().backward()
+ref = {{k: p.grad.clone() for k, p in model.named_parameters()}}
+model.zero_grad(set_to_none=True)
+ar = D.GradAllReduce(model.parameters(), bucket_bytes=1 << 20)
+ar.arm()
+loss().backward()  # buckets pack and all-reduce from the hooks as their gradients land
+in_hooks = ar.launched_in_hooks
+ar()
+torch.cuda.synchronize()
+same = all(torch.equal(p.grad, ref[k]) for k, p in model.named_parameters())
+json.dump({{"backend": torch.distributed.get_backend(), "buckets": len(ar.buckets), "in_hooks": in_hooks,
+            "equal": same, "n_glob": n_glob}}, open({out!r}, "w"))
+torch.distributed.destroy_process_group()
+'''
+
+
+def test_rccl_world_of_one_grad_allreduce(tmp_path):
+    out = str(tmp_path / "r.json")
+    script = tmp_path / "rccl_worker.py"
+    script.write_text(RCCL_WORKER.format(root=ROOT, kw=KW, out=out))
+    r = _torchrun([str(script)], timeout=300, nproc=1, backend="nccl", AEROGNN_DIST_FORCE="1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.load(open(out))
+    print(d)
+    assert d["backend"] == "nccl" and d["equal"], d
+    assert d["buckets"] >= 2 and d["in_hooks"] >= 1, d  # the armed path ran, not only the tail call
+    assert d["n_glob"] == 24 * 16 * 4  # y is [N, 4]
+
+
+def test_bench_rccl_world_of_one_json():
+    r = _torchrun(["bench.py", "--gpus", "1", "--config", "small", "--steps", "2", "--warmup", "1",
+                   "--no-cpu-baseline"], timeout=400, nproc=1, backend="nccl", AEROGNN_DIST_FORCE="1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    print(d["collective"], d["value"])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["collective"]["backend"] == "nccl" and d["collective"]["launched_in_hooks"] >= 1, d["collective"]

@@ -156,6 +156,56 @@ def test_c2_layer_fp32_vs_oracle():
         assert r <= 1e-5 and m <= 1e-5
 
 
+@pytest.mark.parametrize("trick", [False, True])
+def test_c2_layer_fp32_fwd_bwd_vs_oracle(trick):
+    """One fp32 MeshGraphNetLayer at C2 size, forward AND backward, against the CPU oracle's
+    float64 autograd: every output, input gradient and parameter gradient at the 1e-5 bar
+    (rel-L2; outputs and input gradients also max-element). trick=False is the concat edge MLP
+    (mgnLayer.py:10-49): hand-written kernels only (gathered-operand agn_wgrad for W_0's x_src /
+    x_dst blocks, agn_segment_sum2 for dx + scatter(d x_src) + scatter(d x_dst)). Inputs are
+    conditioned away from ReLU kinks (tests/kinkfree.py: rows re-drawn, none dropped)."""
+    from kinkfree import kink_free
+    from models.mgnLayer import MeshGraphNetLayer
+    from oracle import refcpu as R
+    m = _mesh(400, 250)  # C2: 100,000 nodes / 598,400 edges
+    N, E = m["x"].shape[0], m["edge_index"].shape[1]
+    torch.manual_seed(0)
+    layer = MeshGraphNetLayer(128, 128, 128, 2, 2, do_concat_trick=trick)
+    g = torch.Generator(device="cpu").manual_seed(4)
+    x = torch.randn(N, 128, generator=g)
+    e = torch.randn(E, 128, generator=g)
+    gxo = torch.randn(N, 128, generator=g)
+    geo = torch.randn(E, 128, generator=g)
+    p64 = {f"L.{k}": v.double() for k, v in layer.state_dict().items()}
+    cfg = R.cfg_from_kwargs(num_hidden_layers_node_processor=2, num_hidden_layers_edge_processor=2,
+                            do_concat_trick=trick, aggregation="add")
+    ei = m["edge_index"]
+    n = kink_free(lambda xx, ee: R.gmp_layer(p64, "L", xx, ee, ei, cfg), x, e, g)
+    print(f"kink-free inputs: {n} rows re-drawn of {N + E}")
+    p = {k: v.clone().requires_grad_(True) for k, v in p64.items()}
+    xr_in, er_in = x.double().requires_grad_(True), e.double().requires_grad_(True)
+    xr, er = R.gmp_layer(p, "L", xr_in, er_in, ei, cfg)
+    torch.autograd.backward([xr, er], [gxo.double(), geo.double()])
+    layer = layer.to(DEV)
+    xg, eg = x.to(DEV).requires_grad_(True), e.to(DEV).requires_grad_(True)
+    xo, eo = layer(xg, eg, ei.to(DEV))
+    torch.autograd.backward([xo, eo], [gxo.to(DEV), geo.to(DEV)])
+    torch.cuda.synchronize()
+    pairs = [("x'", xo, xr), ("e'", eo, er), ("dx", xg.grad, xr_in.grad), ("de", eg.grad, er_in.grad)]
+    pairs += [(n, q.grad, p[f"L.{n}"].grad) for n, q in layer.named_parameters()]
+    worst = ("", 0.0)
+    for name, got, ref in pairs:
+        got, ref = got.detach().cpu().double(), ref.detach()
+        r = rel_l2(got, ref)
+        mx = float((got - ref).abs().max()) / max(float(ref.abs().max()), 1e-30)
+        if name in ("x'", "e'", "dx", "de"):
+            print(f"C2 {'sum' if trick else 'concat'} layer {name}: rel-L2 {r:.2e}, max-elem {mx:.2e}")
+            assert r <= 1e-5 and mx <= 1e-5, (name, r, mx)
+        worst = max(worst, (name, r), key=lambda t: t[1])
+    print(f"C2 {'sum' if trick else 'concat'} layer param grads worst rel-L2 {worst[1]:.2e} ({worst[0]})")
+    assert worst[1] <= 1e-5, worst
+
+
 def test_c3_pooling_maps_bitexact_vs_oracle():
     from models.bsms_mgn import BiStridedMeshGraphNet
     from oracle import refcpu as R

@@ -46,6 +46,54 @@ def test_wgrad_split_columns():
     assert rel_l2(dw, ref) <= 1e-6
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,N,K", [(1, 5, 128), (70001, 3000, 128), (999, 50, 6)])
+def test_wgrad_gathered_operand(dtype, rows, N, K):
+    """agn_wgrad's xidx: X row r = x[idx[r]] (the concat edge MLP's x_src / x_dst blocks) equals
+    the product with the materialised x[idx] (ragged stage, repeated indices, narrow K)."""
+    from aerognn.core import WGrad
+    g = torch.Generator(device="cpu").manual_seed(rows + K)
+    G = torch.randn(rows, 128, generator=g).to(DEV, dtype)
+    x = torch.randn(N, K, generator=g).to(DEV, dtype)
+    idx = torch.randint(0, N, (rows,), generator=g, dtype=torch.int32).to(DEV)
+    dw = torch.empty(128, K, dtype=torch.float32, device=DEV)
+    db = torch.empty(128, dtype=torch.float32, device=DEV)
+    dw2 = torch.empty_like(dw)
+    wg = WGrad()
+    wg.add(G, x, dw, db, xidx=idx)
+    wg.add(G, x.index_select(0, idx.long()).contiguous(), dw2)
+    wg.run()
+    assert torch.equal(dw, dw2)  # same operand values, same order: bitwise
+    ref = G.double().t() @ x.double()[idx.long()]
+    assert rel_l2(dw, ref) <= 1e-6 and rel_l2(db, G.double().sum(0)) <= 1e-6
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("with_base", [True, False])
+def test_segment_sum2_vs_torch(dtype, with_base):
+    """agn_segment_sum2: out = base + sum over src groups (via perm) + sum over dst groups, in
+    place over base, against index_add_ in fp64 (empty groups, isolated nodes)."""
+    from aerognn.core import segment_sum2
+    from aerognn.graph import Level
+    g = torch.Generator(device="cpu").manual_seed(7)
+    N, E, H = 2000, 9000, 128
+    ei = torch.randint(0, N - 100, (2, E), generator=g)  # nodes >= N-100 have no edges
+    lv = Level.from_edge_index(ei.to(DEV), N)
+    ds = torch.randn(E, H, generator=g)
+    dd = torch.randn(E, H, generator=g)
+    base = torch.randn(N, H, generator=g)
+    # ds / dd rows are the level's (CSC-ordered) edges: row j belongs to src[j] and dst[j]
+    src, dst = lv.src.long().cpu(), lv.dst.long().cpu()
+    ref = (base.double() if with_base else torch.zeros(N, H, dtype=torch.float64))
+    ref = ref.index_add(0, src, ds.double()).index_add(0, dst, dd.double())
+    b = base.to(DEV, dtype)
+    out = b if with_base else torch.empty(N, H, dtype=dtype, device=DEV)
+    segment_sum2(N, H, b if with_base else None, (lv.rowptr_src, lv.perm_src, ds.to(DEV, dtype)),
+                 (lv.rowptr, None, dd.to(DEV, dtype)), out)
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    assert rel_l2(out.cpu(), ref) <= tol
+
+
 @pytest.mark.parametrize("nw,n", [(1, 256), (47000, 256), (5, 7)])
 def test_colsum(nw, n):
     from aerognn.core import colsum_rows
