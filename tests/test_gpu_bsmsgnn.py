@@ -1,7 +1,8 @@
 """GPU parity of the stale BSMS-GNN operators (libaerognn) against the CPU oracle restated from
 SURVEY Appendix A (oracle/bsmsgnn.py; parity with the reference itself is unpinned).
 Integer work (BFS distances, seeds, selections, sub-graphs) bit-exact; fp32 outputs rel-L2
-<= 1e-5; gradients rel-L2 <= 1e-4 (fp32, different valid summation orders).
+and max-element <= 1e-5 (the main model's forward bar); gradients rel-L2 <= 1e-4 (fp32, different
+valid summation orders).
 """
 import os
 
@@ -9,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_util import rel_l2
+from golden_util import max_rel, rel_l2
 
 pytestmark = pytest.mark.gpu
 os.environ.setdefault("AEROGNN_MEMLOG", "0")
@@ -100,6 +101,13 @@ def test_unpool_fwd_bwd():
     assert torch.equal(out3, ref3)
 
 
+def _fwd(got, ref, tol=1e-5):
+    """The main model's forward bar (test_gpu_parity._fwd_ok): rel-L2 AND max-element <= tol."""
+    got, ref = got.detach().float().cpu(), ref.detach().float()
+    r, m = rel_l2(got, ref), max_rel(got, ref)
+    assert r <= tol and m <= tol, (r, m)
+
+
 def _params(mod):
     return {k: v.detach().cpu().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
 
@@ -119,8 +127,8 @@ def test_weighted_edge_conv(aggr):
     out_r, w_r = _wec_ref(O, p, xr, ei, pos, aggr)
     xg = x.to(DEV).requires_grad_(True)
     out, w = wec(xg, ei.to(DEV), pos.to(DEV))
-    assert rel_l2(out.detach().cpu(), out_r.detach()) <= 1e-5
-    assert rel_l2(w.detach().cpu(), w_r.detach()) <= 1e-5
+    _fwd(out, out_r)
+    _fwd(w, w_r)
     go = torch.randn(out.shape, generator=g)
     gw = torch.randn(w.shape, generator=g)
     (out_r * go).sum().backward(retain_graph=True)
@@ -138,7 +146,7 @@ def test_weighted_edge_conv(aggr):
     xg2 = x.to(DEV).requires_grad_(True)
     out2, w2 = wec(xg2, ei.to(DEV), pos.to(DEV), edge_weights=wd, compute_weights=False)
     assert w2 is wd
-    assert rel_l2(out2.detach().cpu(), ref2.detach()) <= 1e-5
+    _fwd(out2, ref2)
     (ref2 * go).sum().backward()
     (out2 * go.to(DEV)).sum().backward()
     assert rel_l2(xg2.grad.cpu(), xr2.grad) <= 1e-4
@@ -166,8 +174,8 @@ def test_gmp_fwd_bwd():
     xo_r, eo_r = O.gmp(p, "g", xr, er, ei)
     xg, eg = x.to(DEV).requires_grad_(True), e.to(DEV).requires_grad_(True)
     xo, eo = gmp(xg, eg, ei.to(DEV))
-    assert rel_l2(xo.detach().cpu(), xo_r.detach()) <= 1e-5
-    assert rel_l2(eo.detach().cpu(), eo_r.detach()) <= 1e-5
+    _fwd(xo, xo_r)
+    _fwd(eo, eo_r)
     gx, ge = torch.randn(xo.shape, generator=g), torch.randn(eo.shape, generator=g)
     ((xo_r * gx).sum() + (eo_r * ge).sum()).backward()
     ((xo * gx.to(DEV)).sum() + (eo * ge.to(DEV)).sum()).backward()
@@ -194,7 +202,7 @@ def test_bsms_gnn_model_vs_oracle():
     multi_cpu = {k: [t.cpu() if torch.is_tensor(t) else t for t in v] for k, v in multi.items()}
     ref = O.bsms_gnn_forward(p, m["x"], m["edge_attr"], multi_cpu, 2)
     pred = model(m["x"].to(DEV), m["edge_attr"].to(DEV), m["edge_index"].to(DEV), multi_data=multi)
-    assert rel_l2(pred.detach().cpu(), ref.detach()) <= 1e-5
+    _fwd(pred, ref)
     torch.nn.functional.mse_loss(ref, m["y"]).backward()
     torch.nn.functional.mse_loss(pred, m["y"].to(DEV)).backward()
     errs = []
@@ -204,8 +212,9 @@ def test_bsms_gnn_model_vs_oracle():
             continue
         errs.append(rel_l2(prm.grad.cpu(), p[name].grad))
     errs = np.array(errs)
-    # deep fp32 model: ReLU kinks move single parameters; gate the distribution (tests/test_gpu_parity.py)
-    assert np.median(errs) <= 1e-5 and errs.max() <= 1e-2, (np.median(errs), errs.max())
+    print(f"BSMS-GNN param grads rel-L2: median {np.median(errs):.2e}, max {errs.max():.2e}")
+    # the main model's parameter-gradient bar (test_gpu_parity.GPAR): every parameter <= 5e-5
+    assert errs.max() <= 5e-5, (np.median(errs), errs.max())
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])

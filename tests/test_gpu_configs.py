@@ -6,7 +6,7 @@ of the drop-in boundary.
 * C4 (BSMS-4 over PyG-collated micro-batches of ellipsoid(400,250) meshes): the pooling maps of
   one full 8-mesh micro-batch bit-exact at all three levels, and the fp32 forward of a 2-mesh
   batch vs the oracle at 1e-5.
-* C5 (5M nodes / 29,990,000 edges, 6 levels, bf16): the first two pooling levels bit-exact vs the
+* C5 (5M nodes / 29,990,000 edges, 6 levels, bf16): all five pooling levels bit-exact vs the
   oracle, and the full-size bf16 forward deterministic and finite.
 * bf16: the whole C3 architecture in bf16 vs the fp32 oracle (reported; SURVEY §8 does not gate
   it), and the reference's own bf16 mode (`model.to(torch.bfloat16)`: bf16 parameters) vs the
@@ -30,6 +30,8 @@ pytestmark = pytest.mark.gpu
 os.environ.setdefault("AEROGNN_MEMLOG", "0")
 DEV = "cuda"
 FWD = 1e-5
+# 3x the measured full-size bf16-vs-fp32 rel-L2, 8.92e-3 (profiles/r3_gpu_evidence_tests.log)
+C3_BF16_GATE = 2.7e-2
 
 
 def _mesh(nu, nv, seed=0):
@@ -137,10 +139,10 @@ def test_c4_two_meshes_fp32_forward_vs_oracle():
 
 
 # ------------------------------------------------------------------------------ C5
-def test_c5_pooling_maps_first_two_levels_bitexact():
+def test_c5_pooling_maps_all_five_levels_bitexact():
     t = _mesh(2500, 2000)
     assert (t["x"].shape[0], t["edge_index"].shape[1]) == (5000000, 29990000)
-    _levels_vs_oracle(t, 2, width=1)
+    _levels_vs_oracle(t, 5, width=1)  # the 6-level hierarchy: every one of its 5 poolings
 
 
 def test_c5_bf16_forward_deterministic_finite():
@@ -181,7 +183,26 @@ def test_c3_architecture_bf16_vs_fp32_oracle_reported():
     r32, rbf = rel_l2(p32.float().cpu(), ref), rel_l2(pbf.float().cpu(), ref)
     print(f"BSMS-4 (15 layers, H=128) on 6,000 nodes: fp32 rel-L2 {r32:.2e}, bf16 rel-L2 {rbf:.2e} vs fp32 oracle")
     assert r32 <= FWD
-    assert np.isfinite(rbf) and rbf < 0.25
+    # 3x the measured 8.84e-3 (profiles/r2_gpu_tests_verbose.log): a regression gate, not a spec
+    assert np.isfinite(rbf) and rbf <= 2.7e-2
+
+
+def test_c3_full_size_bf16_vs_fp32_hip():
+    """Whole-model bf16 error at the headline size (1M nodes / 5,996,000 edges, BSMS-4, 15
+    layers): bf16 activations against the fp32 HIP path on the same model and mesh. The fp32 path
+    is oracle-pinned at the 1e-5 bar at C2 and C4 sizes (tests above); here it is the reference
+    for the bf16 error the headline metric is measured at."""
+    from models.bsms_mgn import BiStridedMeshGraphNet
+    t = {k: v.to(DEV) for k, v in _mesh(1000, 1000).items()}
+    torch.manual_seed(0)
+    model = BiStridedMeshGraphNet(6, 4, 4, **_kw()).to(DEV)
+    with torch.no_grad():
+        p32 = model(t["x"], t["edge_attr"], t["edge_index"], pos=t["pos"]).double()
+        pbf = model(t["x"].bfloat16(), t["edge_attr"].bfloat16(), t["edge_index"], pos=t["pos"]).double()
+    r = float((pbf - p32).norm() / p32.norm())
+    mx = float((pbf - p32).abs().max() / p32.abs().max())
+    print(f"C3 full size BSMS-4: bf16 vs fp32 HIP rel-L2 {r:.2e}, max-elem {mx:.2e}")
+    assert np.isfinite(r) and r <= C3_BF16_GATE
 
 
 def test_reference_bf16_mode_layer():
