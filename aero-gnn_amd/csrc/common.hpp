@@ -99,6 +99,14 @@ AGN_DEV uint32_t pack2(float x, float y) { return __builtin_bit_cast(uint32_t, b
 AGN_DEV float lo_bf16(uint32_t u) { return __uint_as_float(u << 16); }
 AGN_DEV float hi_bf16(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 // the same for either 16-bit storage type (T = bf16 / f16; fp16 converts, bf16 shifts)
+// ReLU of two packed 16-bit floats as int16 max with 0 (v_pk_max_i16): a set sign bit (negative,
+// -0) gives +0, everything else is kept. relu(round(x)) == round(relu(x)) bit for bit for every
+// non-NaN x (a value that rounds to -0 was negative), and a NaN stays NaN as in torch.relu,
+// where fmaxf(NaN, 0) would give 0. Replaces the canonicalising v_max_f32 pair per element.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+AGN_DEV uint32_t relu_pk16(uint32_t x) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, x), s16x2{0, 0}));
+}
 template <typename T> AGN_DEV uint32_t pack2t(float x, float y);
 template <> AGN_DEV uint32_t pack2t<bf16>(float x, float y) { return pack2(x, y); }
 template <> AGN_DEV uint32_t pack2t<f16>(float x, float y) { return __builtin_bit_cast(uint32_t, f16x2{(f16)x, (f16)y}); }
@@ -405,9 +413,14 @@ template <int NR> struct BOp<bf16, NR> {
   template <int NT>
   AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
 #pragma unroll
-    for (int i = 0; i < NR / 8; ++i)
+    for (int i = 0; i < NR / 8; ++i) {
+      u32x4 w;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[i][j] = (bf16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
+      for (int k = 0; k < 4; ++k)
+        w[k] = relu_pk16(pack2(acc[(8 * i + 2 * k) / 16][(8 * i + 2 * k) % 16],
+                               acc[(8 * i + 2 * k + 1) / 16][(8 * i + 2 * k + 1) % 16]));
+      u[i] = __builtin_bit_cast(bf16x8, w);
+    }
   }
   // registers 8i..8i+7 (acc order) as floats
   AGN_DEV void get8(float (&o)[8], int i) const {
@@ -449,9 +462,14 @@ template <int NR> struct BOp<f16, NR> {
   template <int NT>
   AGN_DEV void set_relu(const f32x16 (&acc)[NT]) {
 #pragma unroll
-    for (int i = 0; i < NR / 8; ++i)
+    for (int i = 0; i < NR / 8; ++i) {
+      u32x4 w;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[i][j] = (f16)fmaxf(acc[(8 * i + j) / 16][(8 * i + j) % 16], 0.f);
+      for (int k = 0; k < 4; ++k)
+        w[k] = relu_pk16(pack2t<f16>(acc[(8 * i + 2 * k) / 16][(8 * i + 2 * k) % 16],
+                                     acc[(8 * i + 2 * k + 1) / 16][(8 * i + 2 * k + 1) % 16]));
+      u[i] = __builtin_bit_cast(f16x8, w);
+    }
   }
   AGN_DEV void get8(float (&o)[8], int i) const {
 #pragma unroll

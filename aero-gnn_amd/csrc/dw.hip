@@ -139,7 +139,8 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
 }
 
 // grid: x = row chunk (split), y = M block * nKb + K block, z = desc
-template <typename T>
+// XG: some desc has a gathered X (xidx); a separate instantiation keeps the plain path free of it
+template <typename T, bool XG>
 __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   StageRegs<T> rg, rx;
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
-    rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled, d.xidx);
+    rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled, XG ? d.xidx : nullptr);
   }
   for (int r0 = rbeg; r0 < rend; r0 += DW_ROWS) {
     __syncthreads();
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     __syncthreads();
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
-      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, d.xidx);
+      rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, XG ? d.xidx : nullptr);
     }
     if (d.db_partial && kb == 0) {
       const int col = threadIdx.x & (DW_BLK - 1), q = threadIdx.x >> 7;
@@ -347,7 +348,7 @@ int wgrad_resident() {
     int dev = 0, ncu = 256, per = 3;
     hipDeviceProp_t p;
     if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&p, dev) == hipSuccess) ncu = p.multiProcessorCount;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wgrad_kernel<bf16>, DW_THREADS, 0) != hipSuccess || per < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wgrad_kernel<bf16, false>, DW_THREADS, 0) != hipSuccess || per < 1)
       per = 3;
     resident = ncu * per;
   }
@@ -410,10 +411,18 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   }
   (void)total;
   dim3 grid(ns, maxblk, bb.n);
-  if (dtype == AGN_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16>, grid, dim3(DW_THREADS), 0, st, bb, ns);
-  else if (dtype == AGN_F16) hipLaunchKernelGGL(wgrad_kernel<f16>, grid, dim3(DW_THREADS), 0, st, bb, ns);
-  else if (dtype == AGN_F32) hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(DW_THREADS), 0, st, bb, ns);
+  bool xg = false;
+  for (int i = 0; i < bb.n; ++i) xg = xg || bb.d[i].xidx != nullptr;
+#define AGN_WG(T)                                                                             \
+  do {                                                                                        \
+    if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns); \
+    else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);   \
+  } while (0)
+  if (dtype == AGN_BF16) AGN_WG(bf16);
+  else if (dtype == AGN_F16) AGN_WG(f16);
+  else if (dtype == AGN_F32) AGN_WG(float);
   else return AGN_E_DTYPE;
+#undef AGN_WG
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
   return launch_status();
 }
