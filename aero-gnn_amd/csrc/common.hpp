@@ -148,19 +148,24 @@ AGN_DEV void load8_w(float (&o)[8], const float* rowp, int i, int h) {
 // one wave touches per chunk step all fall into the same 4 banks (8-way conflicts, measured
 // 1.6e8 SQ_LDS_BANK_CONFLICT cycles per 3 edge forwards); 288 B spreads them over 64 banks.
 constexpr int STG_PAD = 2;
+// split form: tile_load_issue puts the tile's global loads in flight (32 registers of raw chunks),
+// tile_load_finish routes them through the staging rows; other work can sit in between
 template <int NC>
-AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC + STG_PAD], int lane,
-                              int ldc = NC) {
+AGN_DEV void tile_load_issue(uint4 (&raw)[NC / 2], const bf16* tile_base, int nvalid, int lane, int ldc = NC) {
   static_assert(NC >= 8 && NC <= 64, "staged tile I/O needs 8..64 chunks per row");
   constexpr int PER = 64 / NC;  // rows covered by one 1-KB instruction
-  const int c = lane & 31, h = lane >> 5;
+  static_assert(32 / PER == NC / 2, "raw chunk count");
   const uint4* gb = reinterpret_cast<const uint4*>(tile_base);
-  uint4 raw[32 / PER];
 #pragma unroll
   for (int k = 0; k < 32 / PER; ++k) {
     const int q = lane + 64 * k, r = q / NC;
     raw[k] = (r < nvalid) ? gb[(size_t)r * ldc + q % NC] : uint4{0u, 0u, 0u, 0u};
   }
+}
+template <int NC>
+AGN_DEV void tile_load_finish(uint4 (&mine)[NC / 2], const uint4 (&raw)[NC / 2], uint4 (*stg)[NC + STG_PAD], int lane) {
+  constexpr int PER = 64 / NC;
+  const int c = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
 #pragma unroll
@@ -176,6 +181,13 @@ AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int 
     }
     __builtin_amdgcn_wave_barrier();
   }
+}
+template <int NC>
+AGN_DEV void tile_load_chunks(uint4 (&mine)[NC / 2], const bf16* tile_base, int nvalid, uint4 (*stg)[NC + STG_PAD], int lane,
+                              int ldc = NC) {
+  uint4 raw[NC / 2];
+  tile_load_issue<NC>(raw, tile_base, nvalid, lane, ldc);
+  tile_load_finish<NC>(mine, raw, stg, lane);
 }
 template <int NC>
 AGN_DEV void tile_store_chunks(const uint4 (&mine)[NC / 2], bf16* tile_base, int nvalid, uint4 (*stg)[NC + STG_PAD], int lane,
@@ -359,6 +371,12 @@ AGN_DEV void load8_tiled(float (&v)[8], const T* base, int i, int row, int h) {
 // Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
 // rows) above the MFMA chain, where they would sit live in registers across every layer.
 AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
+// a value behind a compiler barrier: per-lane offsets derived from it are recomputed where used
+// instead of being hoisted out of a tile loop (where they would sit in registers and spill)
+AGN_DEV int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
 // feature index held in register rho by lane half h (acc layout)
 AGN_DEV int feat_of(int rho, int h) { return 8 * (rho >> 2) + 4 * h + (rho & 3); }

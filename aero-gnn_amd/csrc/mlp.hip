@@ -554,6 +554,10 @@ constexpr int RES_MAXL = 4;
 // live registers spill (measured: 2.55 -> 2.88 ms per launch with de staging), so both stay off
 constexpr bool kStageGradIn = false;
 constexpr bool kStageGradOut = false;
+#ifndef AGN_EARLY_E
+#define AGN_EARLY_E 0
+#endif
+constexpr bool kEarlyE = AGN_EARLY_E;
 
 template <typename T, int NT>
 constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
@@ -578,6 +582,22 @@ struct ResTiles {
   }
 };
 
+// Diagnostic phase clocks of the resident edge forward (built with -DAGN_FWD_STAMPS into the
+// separate stamps library only): the 8 waves of block 0 record s_memtime at 10 points of their
+// first 8 tiles into agn_fwd_stamps[(wave * 8 + tile) * 16 + point].
+#ifdef AGN_FWD_STAMPS
+__device__ unsigned long long* agn_fwd_stamps;
+#define FWD_STAMP(k)                                                                                   \
+  do {                                                                                                 \
+    if (agn_fwd_stamps && blockIdx.x == 0 && lane == 0 && ntile < 8)                                   \
+      agn_fwd_stamps[((threadIdx.x >> 6) * 8 + ntile) * 16 + (k)] = __builtin_amdgcn_s_memtime();      \
+  } while (0)
+#else
+#define FWD_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
@@ -590,8 +610,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int c = lane & 31, h = lane >> 5;
+  const int lane0 = threadIdx.x & 63;
   const int ntiles = (a.rows + 31) / 32;
   const agn_seg& sg = a.seg[0];
   const ResTiles tw(ntiles, threadIdx.x >> 6);
@@ -599,17 +618,31 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   // projection-row gathers issue together with its e loads (one memory latency per tile, not two)
   int nsrc = 0, ndst = 0;
   if (a.proj && tw.first < tw.end) {
-    const int r0 = min(tw.first * 32 + c, a.rows - 1);
+    const int r0 = min(tw.first * 32 + (lane0 & 31), a.rows - 1);
     nsrc = a.src[r0];
     ndst = a.dst[r0];
   }
+#ifdef AGN_FWD_STAMPS
+  int ntile = 0;
+#endif
   for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
+    // the lane id behind a barrier each tile: lane-derived offsets (row addresses, staging and
+    // weight-fragment offsets) are recomputed per tile instead of being hoisted and kept live
+    const int lane = opaque_v(lane0);
+    const int c = lane & 31, h = lane >> 5;
+    FWD_STAMP(0);
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
     f32x16 acc[NT];
     BOp<T, NR> b;
+    // kEarlyE: the e tile's loads go out before the projection rows are waited on (their
+    // latencies overlap); off, the rows are gathered and summed first (two latencies per tile)
+    const bool staged_in = sg.ld == H;
+    uint4 eraw[NR / 8];
+    if (kEarlyE && staged_in)
+      tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32, lane);
     if (a.proj) {
       const int cs = nsrc, cd = ndst;
       if (tile + tw.step < tw.end) {
@@ -631,12 +664,15 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     } else {
       acc_bias_lds<NT>(acc, pv[0], h);
     }
+    FWD_STAMP(1);
     {
       float v[NR];
-      if (sg.ld == H) {  // coalesced 1-KB loads through the wave's LDS staging rows
+      if (staged_in) {  // coalesced 1-KB loads through the wave's LDS staging rows
+        if (!kEarlyE)
+          tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                                 lane);
         uint4 mine[NR / 8];
-        tile_load_chunks<H / 8>(mine, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
-                                stg[threadIdx.x >> 6], lane);
+        tile_load_finish<H / 8>(mine, eraw, stg[threadIdx.x >> 6], lane);
 #pragma unroll
         for (int i = 0; i < NR / 8; ++i) {
           float o[8];
@@ -653,7 +689,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     // operand instead of re-reading the row in the epilogue
     const bool res_in = a.resid == sg.ptr && a.out_ld == sg.ld;
     const BOp<T, NR> e0 = b;
+    FWD_STAMP(2);
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
+    FWD_STAMP(3);
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
@@ -664,7 +702,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       if (a.mask[l - 1]) store_relu_mask<T, NR>(a.mask[l - 1], b, tile, lane);
       cbarrier();
       acc_bias_lds<NT>(acc, pv[l], h);
+      FWD_STAMP(4 + 2 * (l - 1));
       gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
+      FWD_STAMP(5 + 2 * (l - 1));
     }
     // epilogue: LayerNorm, residual, store (8 features per lane at a time)
     float mean = 0.f, rstd = 1.f;
@@ -687,6 +727,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         a.stats[2 * (size_t)row + 1] = rstd;
       }
     }
+    FWD_STAMP(10);
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * H : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
@@ -721,9 +762,14 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       if (stage_out) ob[i] = pack8_w(v, h);
       else store8_w(op, i, h, v, valid);
     }
+    FWD_STAMP(11);
     if (stage_out)  // 8-row passes through LDS: every store instruction writes 1 KB contiguous
       tile_store_chunks<H / 8>(ob, reinterpret_cast<T*>(a.out) + (size_t)tile * 32 * H, a.rows - tile * 32,
                                stg[threadIdx.x >> 6], lane);
+    FWD_STAMP(12);
+#ifdef AGN_FWD_STAMPS
+    ++ntile;
+#endif
   }
 }
 
@@ -1106,6 +1152,12 @@ bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
          din_ok && a->rows >= 64 * 1024;
 }
 }  // namespace
+
+#ifdef AGN_FWD_STAMPS
+extern "C" int agn_debug_fwd_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(agn_fwd_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" {
 
