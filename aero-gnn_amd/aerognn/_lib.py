@@ -95,6 +95,7 @@ _lib = None
 # finer tag (edge_fwd, node_bwd, ...). Nothing is recorded when PROF is None.
 LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_partials", "agn_wgrad", "agn_colsum",
             "agn_segment_sum", "agn_segment_sum2", "agn_gather_rows", "agn_radix_sort_u64", "agn_row_ptr", "agn_row_ptr_i64",
+            "agn_iota_keys", "agn_level_index",
             "agn_exclusive_scan_i32", "agn_pool_sort_keys", "agn_pool_assign", "agn_pool_edge_candidates",
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
@@ -171,6 +172,8 @@ def lib():
             "agn_radix_sort_u64": (i32, [vp, vp, i32, i32, vp, vp, vp, vp]),
             "agn_row_ptr": (i32, [vp, i32, i32, vp, vp]),
             "agn_row_ptr_i64": (i32, [vp, i32, i32, vp, vp]),
+            "agn_iota_keys": (i32, [i32, vp, vp, vp, vp, vp]),
+            "agn_level_index": (i32, [i32, vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp]),
             "agn_scan_temp_bytes": (C.c_size_t, [i32]),
             "agn_exclusive_scan_i32": (i32, [vp, vp, i32, vp, vp, vp]),
             "agn_pool_sort_keys": (i32, [i32, vp, vp, i32, vp, vp, vp]),

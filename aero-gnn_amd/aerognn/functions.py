@@ -237,6 +237,37 @@ class MLPFn(torch.autograd.Function):
         return (dx, None, None, None, *grads)
 
 
+class PermuteRowsFn(torch.autograd.Function):
+    """y = x[perm] for a permutation of rows (caller edge order <-> CSC order of a level): a row
+    gather on agn_gather_rows both ways (the backward gathers by the inverse permutation)."""
+
+    @staticmethod
+    def forward(ctx, x, perm32, inv32):
+        require_device(x)
+        x = _c(x)
+        ctx.inv32 = inv32
+        return gather_rows(x.shape[0], x.shape[1], perm32, x, torch.empty_like(x))
+
+    @staticmethod
+    def backward(ctx, g):
+        g = _c(g)
+        return gather_rows(g.shape[0], g.shape[1], ctx.inv32, g, torch.empty_like(g)), None, None
+
+
+def permute_rows(x, perm32, inv32):
+    return PermuteRowsFn.apply(x, perm32, inv32)
+
+
+def to_csc(x, lv):
+    """Rows in the caller's edge order -> the level's CSC order (x[lv.perm])."""
+    return PermuteRowsFn.apply(x, lv.perm32, lv.inv32)
+
+
+def from_csc(x, lv):
+    """Rows in the level's CSC order -> the caller's edge order (x[lv.perm_inv])."""
+    return PermuteRowsFn.apply(x, lv.inv32, lv.perm32)
+
+
 # --------------------------------------------------------------------------- GMP layer
 class LayerSpec:
     """Binds reference blocks (mgnLayer.py:10-213) to packed operands.

@@ -35,16 +35,19 @@ def radix_sort(keys_u64: torch.Tensor, vals_i32: torch.Tensor, bits: int):
     return keys_u64, vals_i32
 
 
-def group_by(keys_i32: torch.Tensor, nrows: int):
-    """Stable grouping of positions 0..n-1 by key: returns (perm int32, rowptr int32 [nrows+1])."""
-    n = keys_i32.numel()
-    dev = keys_i32.device
-    k = keys_i32.to(I64)
-    v = torch.arange(n, dtype=I32, device=dev)
+def group_by(keys: torch.Tensor, nrows: int):
+    """Stable grouping of positions 0..n-1 by key (int32, or an int64 row such as edge_index[1]):
+    returns (perm int32, rowptr int32 [nrows+1])."""
+    n = keys.numel()
+    dev = keys.device
+    k = torch.empty(n, dtype=I64, device=dev)
+    v = torch.empty(n, dtype=I32, device=dev)
+    if n:
+        k32, k64 = (keys, None) if keys.dtype == I32 else (None, keys)
+        check(L.lib().agn_iota_keys(n, ptr(k32), ptr(k64), ptr(k), ptr(v), stream()), "iota_keys")
     radix_sort(k, v, _bits(nrows))
-    ks = k.to(I32)
     rp = torch.empty(nrows + 1, dtype=I32, device=dev)
-    check(L.lib().agn_row_ptr(ptr(ks), n, nrows, ptr(rp), stream()), "row_ptr")
+    check(L.lib().agn_row_ptr_i64(ptr(k), n, nrows, ptr(rp), stream()), "row_ptr_i64")
     return v, rp
 
 
@@ -85,15 +88,23 @@ class Level:
 
     @staticmethod
     def from_edge_index(edge_index: torch.Tensor, N: int) -> "Level":
-        """Reference edge_index [2,E] int64 (any order) -> CSC level (stable by edge id)."""
-        ei = edge_index
+        """Reference edge_index [2,E] int64 (any order) -> CSC level (stable by edge id), all in
+        libaerognn kernels: radix sort of the receivers, row pointers, one gather pass."""
+        ei = edge_index if edge_index.dtype == I64 and edge_index.stride(1) == 1 else edge_index.to(I64).contiguous()
         E = ei.shape[1]
-        dst_in = ei[1].to(I32)
-        perm32, rowptr = group_by(dst_in, N)
-        perm = perm32.to(I64)
-        src = ei[0].index_select(0, perm).to(I32)
-        dst = ei[1].index_select(0, perm).to(I32)
-        return Level(N, src, dst, rowptr, perm.clone(), perm=perm)
+        dev = ei.device
+        perm32, rowptr = group_by(ei[1], N)
+        src = torch.empty(E, dtype=I32, device=dev)
+        dst = torch.empty(E, dtype=I32, device=dev)
+        perm = torch.empty(E, dtype=I64, device=dev)
+        inv = torch.empty(E, dtype=I64, device=dev)
+        inv32 = torch.empty(E, dtype=I32, device=dev)
+        check(L.lib().agn_level_index(E, ptr(ei), ei.stride(0), ptr(perm32), ptr(src), ptr(dst), ptr(perm), ptr(inv),
+                                      ptr(inv32), stream()), "level_index")
+        lv = Level(N, src, dst, rowptr, perm, perm=perm)
+        lv._perm_inv = inv
+        lv.perm32, lv.inv32 = perm32, inv32  # the row permutations caller <-> CSC (PermuteRowsFn)
+        return lv
 
 
 class Pooling:

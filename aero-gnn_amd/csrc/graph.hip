@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   }
 }
 
-// out[r] = base[r] + (group a of r) + (group b of r): the concat edge MLP's node gradient in one
+// out[r] = (base[r] + (group a of r)) + (group b of r): the concat edge MLP's node gradient in one
 // pass (agn_segment_sum2). Same thread layout and in-order fp32 accumulation as segment_sum_kernel.
 template <typename T>
 AGN_DEV void seg_accum(float (&s)[8], int beg, int end, const int32_t* __restrict__ perm, const T* __restrict__ src,
@@ -134,10 +134,15 @@ __global__ __launch_bounds__(256) void segment_sum2_kernel(int rows, int k, cons
                    ((out_ld % A) == 0) &&
                    ((((uintptr_t)base) | ((uintptr_t)src_a) | ((uintptr_t)src_b) | ((uintptr_t)out)) & 15) == 0;
   for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
+    // each group summed from zero in edge order (segment_sum_kernel's sums), then
+    // (base + sum_a) + sum_b: in fp32 bitwise the two-segment-sum composition it replaces
+    float sa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    seg_accum(sa, ptr_a[r], ptr_a[r + 1], perm_a, src_a, lda, f0, k, vec);
+    seg_accum(sb, ptr_b[r], ptr_b[r + 1], perm_b, src_b, ldb, f0, k, vec);
     float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (base) load8(s, base + (size_t)r * base_ld, f0, k, vec);  // read before this thread's own store (out may alias)
-    seg_accum(s, ptr_a[r], ptr_a[r + 1], perm_a, src_a, lda, f0, k, vec);
-    seg_accum(s, ptr_b[r], ptr_b[r + 1], perm_b, src_b, ldb, f0, k, vec);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = base ? (s[i] + sa[i]) + sb[i] : sa[i] + sb[i];
     store8(out + (size_t)r * out_ld, f0, k, vec, s);
   }
 }
@@ -402,6 +407,30 @@ __global__ void row_ptr_kernel(const int32_t* __restrict__ keys, int n, int nrow
     else hi = mid;
   }
   ptr[v] = lo;
+}
+
+// keys[i] = k32 ? k32[i] : k64[i] as u64 sort keys, vals[i] = i (group_by's stable-sort input)
+__global__ void iota_keys_kernel(int n, const int32_t* __restrict__ k32, const int64_t* __restrict__ k64,
+                                 int64_t* __restrict__ keys, int32_t* __restrict__ vals) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  keys[i] = k32 ? (int64_t)k32[i] : k64[i];
+  vals[i] = i;
+}
+
+// CSC level from edge_index [2][ld] int64 and the receiver-grouping permutation: src / dst int32
+// in CSC order, the permutation as int64 and its inverse (caller edge -> CSC position)
+__global__ void level_index_kernel(int e, const int64_t* __restrict__ ei, int64_t ld, const int32_t* __restrict__ perm,
+                                   int32_t* __restrict__ src, int32_t* __restrict__ dst, int64_t* __restrict__ perm64,
+                                   int64_t* __restrict__ inv64, int32_t* __restrict__ inv32) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= e) return;
+  const int p = perm[i];
+  src[i] = (int32_t)ei[p];
+  dst[i] = (int32_t)ei[ld + p];
+  perm64[i] = p;
+  inv64[p] = i;
+  if (inv32) inv32[p] = i;
 }
 
 __global__ void row_ptr64_kernel(const int64_t* __restrict__ keys, int n, int nrows, int32_t* __restrict__ ptr) {
@@ -780,6 +809,24 @@ int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* tota
 int agn_row_ptr(const int32_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream) {
   if (n < 0 || nrows < 0) return AGN_E_ARG;
   hipLaunchKernelGGL(row_ptr_kernel, g1(nrows + 1), dim3(256), 0, (hipStream_t)stream, sorted_keys, n, nrows, ptr);
+  return launch_status();
+}
+
+int agn_iota_keys(int n, const int32_t* keys32, const int64_t* keys64, int64_t* keys, int32_t* vals, void* stream) {
+  if (n < 0) return AGN_E_ARG;
+  if (n == 0) return 0;
+  if ((!keys32 && !keys64) || !keys || !vals) return AGN_E_ARG;
+  hipLaunchKernelGGL(iota_keys_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, n, keys32, keys64, keys, vals);
+  return launch_status();
+}
+
+int agn_level_index(int e, const int64_t* edge_index, int64_t ld, const int32_t* perm, int32_t* src, int32_t* dst,
+                    int64_t* perm64, int64_t* inv64, int32_t* inv32, void* stream) {
+  if (e < 0) return AGN_E_ARG;
+  if (e == 0) return 0;
+  if (ld < e || !edge_index || !perm || !src || !dst || !perm64 || !inv64) return AGN_E_ARG;
+  hipLaunchKernelGGL(level_index_kernel, g1(e), dim3(256), 0, (hipStream_t)stream, e, edge_index, ld, perm, src, dst,
+                     perm64, inv64, inv32);
   return launch_status();
 }
 

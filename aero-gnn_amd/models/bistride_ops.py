@@ -13,7 +13,7 @@ from torch import nn
 
 from aerognn import bistride as B
 from aerognn.core import require_device
-from aerognn.functions import GMPFn, LayerSpec, UnpoolRowsFn, WECFn, WECGivenFn, WecSpec
+from aerognn.functions import GMPFn, LayerSpec, UnpoolRowsFn, WECFn, WECGivenFn, WecSpec, from_csc, to_csc
 from aerognn.graph import Level
 
 __all__ = ["BistridePooling", "Unpool", "WeightedEdgeConv", "GMP"]
@@ -125,8 +125,8 @@ class GMP(nn.Module):
         """Edges in the caller's order in and out (the level's CSC order internally)."""
         require_device(x, edge_attr, edge_index)
         lv = level if level is not None else _level_of(edge_index, x.shape[0])
-        xo, eo = self.forward_level(x, edge_attr.index_select(0, lv.perm), lv)
-        return xo, eo.index_select(0, lv.perm_inv)
+        xo, eo = self.forward_level(x, to_csc(edge_attr, lv), lv)
+        return xo, from_csc(eo, lv)
 
     def forward_level(self, x, edge_attr_csc, level):
         s = self.spec()

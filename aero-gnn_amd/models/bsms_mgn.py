@@ -225,7 +225,7 @@ class BiStridedMeshGraphNet(nn.Module):
         if run_ids is not None:
             P.cbatch = run_ids[P.cbatch]
         cnode = PoolNodeFn.apply(node_attr, P)
-        cedge_csc = PoolEdgeFn.apply(edge_attr[level.perm], P)
+        cedge_csc = PoolEdgeFn.apply(to_csc(edge_attr, level), P)
         cpos = None
         if pos is not None:
             cpos = PoolNodeFn.apply(pos.float().contiguous(), P).to(pos.dtype)
@@ -245,7 +245,7 @@ class BiStridedMeshGraphNet(nn.Module):
 # bytecode cannot be executed; tests check against oracle/bsmsgnn.py (restated from Appendix A).
 # =====================================================================================
 from aerognn import bistride as _bistride  # noqa: E402
-from aerognn.functions import GatherRowsFn  # noqa: E402
+from aerognn.functions import GatherRowsFn, to_csc  # noqa: E402
 from models.bistride_ops import GMP, Unpool, WeightedEdgeConv, _level_of  # noqa: E402
 
 
@@ -291,7 +291,7 @@ class BSMSGMP(nn.Module):
         cache = {}
         lvs = [_level_of(edge_indices[i], int(num_nodes_list[i]), cache) for i in range(L + 1)]
         # edge latents stay in each level's CSC order inside the U-Net (only x is returned)
-        eas = [ea.index_select(0, lv.perm) for ea, lv in zip(edge_attrs, lvs)]
+        eas = [to_csc(ea, lv) for ea, lv in zip(edge_attrs, lvs)]
         skips, weights = [], []
         for i in range(L):
             x, eas[i] = self.down_gmps[i].forward_level(x, eas[i], lvs[i])

@@ -11,7 +11,7 @@ import os
 import torch
 from torch import nn
 
-from aerognn.functions import EdgeBlockFn, GMPFn, LayerSpec, NodeBlockFn
+from aerognn.functions import EdgeBlockFn, GMPFn, LayerSpec, NodeBlockFn, from_csc, to_csc
 from aerognn.graph import Level
 from models.mlp import MLP
 
@@ -41,8 +41,8 @@ class EdgeBlock(nn.Module):
         s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
         s.pack.update(node_attr.dtype, node_attr.device)
-        out = EdgeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.edge_params())
-        return out[lv.perm_inv]
+        out = EdgeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.edge_params())
+        return from_csc(out, lv)
 
 
 class EdgeBlockSum(nn.Module):
@@ -84,8 +84,8 @@ class EdgeBlockSum(nn.Module):
         s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
         s.pack.update(node_attr.dtype, node_attr.device)
-        out = EdgeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.edge_params())
-        return out[lv.perm_inv]
+        out = EdgeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.edge_params())
+        return from_csc(out, lv)
 
 
 class NodeBlock(nn.Module):
@@ -112,7 +112,7 @@ class NodeBlock(nn.Module):
         s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
         s.pack.update(node_attr.dtype, node_attr.device)
-        return NodeBlockFn.apply(node_attr, edge_attr[lv.perm], lv, s, torch.is_grad_enabled(), *s.node_params())
+        return NodeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.node_params())
 
 
 _MEMLOG = os.environ.get("AEROGNN_MEMLOG", "1") != "0"
@@ -164,5 +164,5 @@ class MeshGraphNetLayer(nn.Module):
 
     def forward(self, node_attr, edge_attr, edge_index):
         lv = _level(edge_index, node_attr.shape[0])
-        x, e = self.forward_level(node_attr, edge_attr[lv.perm], lv)
-        return x, e[lv.perm_inv]
+        x, e = self.forward_level(node_attr, to_csc(edge_attr, lv), lv)
+        return x, from_csc(e, lv)

@@ -205,10 +205,10 @@ int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* s
 /* out[r] = sum (or mean) of src[perm ? perm[j] : j] for j in ptr[r]..ptr[r+1]-1; [rows][k] */
 int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm,
                     const void* src, int src_ld, void* out, int out_ld, int mean, void* stream);
-/* out[r] = base[r] + sum_{j in ptr_a[r]..} src_a[perm_a ? perm_a[j] : j] + sum_{j in ptr_b[r]..}
- * src_b[perm_b ? perm_b[j] : j], fp32 in that order, one rounding: the concat edge MLP's node
- * gradient dx + scatter_add(d x_src, src) + scatter_add(d x_dst, dst) (mgnLayer.py:10-49 backward)
- * in one pass. out may alias base; base NULL = 0. */
+/* out[r] = (base[r] + A[r]) + B[r], A[r] = sum_{j in ptr_a[r]..} src_a[perm_a ? perm_a[j] : j] and
+ * B[r] likewise, each group summed from zero in index order, fp32, one rounding: the concat edge
+ * MLP's node gradient dx + scatter_add(d x_src, src) + scatter_add(d x_dst, dst)
+ * (mgnLayer.py:10-49 backward) in one pass. out may alias base; base NULL = 0. */
 int agn_segment_sum2(int rows, int k, int dtype, const void* base, int base_ld, const int32_t* ptr_a,
                      const int32_t* perm_a, const void* src_a, int lda, const int32_t* ptr_b,
                      const int32_t* perm_b, const void* src_b, int ldb, void* out, int out_ld, void* stream);
@@ -237,6 +237,13 @@ int agn_row_ptr(const int32_t* sorted_keys, int n, int nrows, int32_t* ptr, void
 size_t agn_scan_temp_bytes(int n);
 int agn_exclusive_scan_i32(const int32_t* in, int32_t* out, int n, int32_t* total, int32_t* scratch,
                            void* stream);
+/* group_by's stable-sort input: keys[i] = keys32 ? keys32[i] : keys64[i] (as u64), vals[i] = i */
+int agn_iota_keys(int n, const int32_t* keys32, const int64_t* keys64, int64_t* keys, int32_t* vals, void* stream);
+/* CSC level of a reference edge_index [2][ld] int64 (mgnLayer.py:143-146 receivers `col`): given
+ * perm (int32, edges stably grouped by receiver), src[i] = edge_index[0][perm[i]], dst[i] =
+ * edge_index[1][perm[i]] (int32), perm64[i] = perm[i], inv64[perm[i]] = i (and inv32, if not NULL). */
+int agn_level_index(int e, const int64_t* edge_index, int64_t ld, const int32_t* perm, int32_t* src, int32_t* dst,
+                    int64_t* perm64, int64_t* inv64, int32_t* inv32, void* stream);
 /* same as agn_row_ptr for sorted int64 keys (PyG `batch` vectors) */
 int agn_row_ptr_i64(const int64_t* sorted_keys, int n, int nrows, int32_t* ptr, void* stream);
 

@@ -86,12 +86,21 @@ def test_segment_sum2_vs_torch(dtype, with_base):
     src, dst = lv.src.long().cpu(), lv.dst.long().cpu()
     ref = (base.double() if with_base else torch.zeros(N, H, dtype=torch.float64))
     ref = ref.index_add(0, src, ds.double()).index_add(0, dst, dd.double())
+    if dtype == torch.float32:  # bitwise the composition it replaces: two segment sums, then (base + A) + B
+        from aerognn.core import segment_sum
+        A = segment_sum(N, H, lv.rowptr_src, lv.perm_src, ds.to(DEV), torch.empty(N, H, device=DEV))
+        B = segment_sum(N, H, lv.rowptr, None, dd.to(DEV), torch.empty(N, H, device=DEV))
+        comp = (base.to(DEV) + A) + B if with_base else A + B
     b = base.to(DEV, dtype)
     out = b if with_base else torch.empty(N, H, dtype=dtype, device=DEV)
     segment_sum2(N, H, b if with_base else None, (lv.rowptr_src, lv.perm_src, ds.to(DEV, dtype)),
                  (lv.rowptr, None, dd.to(DEV, dtype)), out)
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert rel_l2(out.cpu(), ref) <= tol
+    if dtype == torch.float32:
+        assert torch.equal(out, comp)
+    if dtype == torch.float32:
+        assert torch.equal(out, comp)
 
 
 @pytest.mark.parametrize("nw,n", [(1, 256), (47000, 256), (5, 7)])

@@ -294,7 +294,24 @@ def test_poolmgn(method):
     pred = model(d["x"].to(DEV), d["edge_attr"].to(DEV), d["edge_index"].to(DEV), batch=d["batch"].to(DEV))
     _fwd_ok(pred, d["pred"])
     torch.nn.functional.mse_loss(pred, d["y"].to(DEV)).backward()
-    _check_param_grads(model, d)
+    # this golden sits on a ReLU kink: the reference's own fp32 gradient of layers.2's edge MLP is
+    # 1.0e-3 from the exact (float64) one, and the HIP fp32 gradient takes the exact side. So every
+    # parameter gradient is gated against the float64 oracle at max(5e-5, 10x the reference's own
+    # fp32-vs-float64 error), and the golden itself at 5e-5 wherever the reference is kink-free.
+    from oracle import refcpu as R
+    cfg = R.cfg_from_kwargs(**m["kwargs"])
+    p64 = {k: v.double().clone().requires_grad_(True) for k, v in params(d).items()}
+    r64 = R.poolmgn_forward(p64, d["x"].double(), d["edge_attr"].double(), d["edge_index"], cfg, batch=d["batch"])
+    torch.nn.functional.mse_loss(r64, d["y"].double()).backward()
+    for name, prm in model.named_parameters():
+        g32, g64 = d.get("gp:" + name), p64[name].grad
+        if g32 is None or g64 is None:
+            continue
+        own = rel_l2(g32.double(), g64)
+        err64 = rel_l2(prm.grad.double().cpu(), g64)
+        assert err64 <= max(GPAR, 10 * own), (name, err64, own)
+        if own <= GPAR / 10:
+            assert rel_l2(prm.grad.float().cpu(), g32.float()) <= GPAR, name
 
 
 @pytest.mark.parametrize("method", ["mean", "max"])
