@@ -655,7 +655,27 @@ AGN_DEV float ln_bwd_out(float g, float gm, float c1, float c2, float xh, float 
 }
 
 // ---------------------------------------------------------------- wave reductions
-AGN_DEV float xor32(float v) { return __shfl_xor(v, 32, 64); }
+// The value a butterfly partner at distance M holds, with VALU cross-lane operations (no LDS
+// round trip, unlike __shfl_xor's ds_bpermute). M = 1, 2: DPP quad_perm (lane ^ M); M = 4: DPP
+// row_half_mirror (lane ^ 7 within 8 lanes: it differs from this lane in bit 2, which is all a
+// reduce step over bit 2 needs; the summation tree changes, not the set summed); M = 8: DPP
+// row_ror:8 (lane ^ 8 within a 16-lane row); M = 16 / 32: v_permlane16_swap / v_permlane32_swap.
+template <int M> AGN_DEV float partner(float v) {
+  const int x = __float_as_int(v);
+  if constexpr (M == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+  else if constexpr (M == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+  else if constexpr (M == 4) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));
+  else if constexpr (M == 8) return __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false));
+  else if constexpr (M == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)x, (uint32_t)x, false, false);
+    return __uint_as_float((__lane_id() & 16) ? r[0] : r[1]);
+  } else {
+    static_assert(M == 32, "butterfly distance");
+    const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)x, false, false);
+    return __uint_as_float((__lane_id() & 32) ? r[0] : r[1]);
+  }
+}
+AGN_DEV float xor32(float v) { return partner<32>(v); }
 
 // Transpose-reduce NR per-lane values over the 32 lanes of each half (lanes c = l & 31).
 // On return lane c holds in v[i] (i < max(NR/32,1)) the 32-lane sum of register
@@ -672,11 +692,11 @@ struct Butterfly {
         for (int i = 0; i < HALF; ++i) {
           const float keep = upper ? v[HALF + i] : v[i];
           const float send = upper ? v[i] : v[HALF + i];
-          v[i] = keep + __shfl_xor(send, M, 64);
+          v[i] = keep + partner<M>(send);
         }
         Butterfly<NR, HALF, M / 2>::run(v, c);
       } else {
-        v[0] += __shfl_xor(v[0], M, 64);
+        v[0] += partner<M>(v[0]);
         Butterfly<NR, 1, M / 2>::run(v, c);
       }
     }

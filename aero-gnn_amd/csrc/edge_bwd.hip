@@ -44,6 +44,10 @@ constexpr int CW = 4;                  // chain waves
 constexpr int NWAVE = 8;               // chain + dW waves
 constexpr int NTHR = 64 * NWAVE;
 constexpr int NSLOT = 3;
+#ifndef AGN_EB_GROUP
+#define AGN_EB_GROUP 2
+#endif
+constexpr int GROUP = AGN_EB_GROUP;  // chain waves per hand-off group (item order, chain_wave)
 constexpr int IMG_B = H * H * 2;       // one 128 x 128 bf16 image (32 KB)
 constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
 constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
@@ -185,7 +189,7 @@ struct Rounds {  // XCD-grouped round walk (blocks b and b + 8 share an XCD and 
 };
 
 // ------------------------------------------------------------------------------ chain wave
-// Item n = (round, L, chain wave, half), n = 24 round + 8 (3 - L) + 2 cw + half: G_L and a_L of
+// Item n = (round, wave group, L, chain wave, half) (chain_wave's nbase): G_L and a_L of
 // rows 16 half .. 16 half + 15 of the wave's tile, as two layout (a) images: unit i of lane
 // (c, hh) = positions 16i + 8hh..+7 (chunk 2i + hh) of row c & 15. A chain wave hands both halves
 // over at once (items n0, n0 + 1): every lane writes, each half into its own slot.
@@ -276,7 +280,13 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int cmax = min(CW, ntiles - rd * CW);
     if (cw >= cmax) continue;
     EB_STAMP(0);
-    const int nbase = rcount * 6 * CW;  // only a workgroup's last round can be partial
+    // Item order within a round: wave group g (waves 2g, 2g+1), then layer, then wave, then half.
+    // The ring hands over one group's whole backward before the other's, so the two groups run
+    // half a tile apart and the hand-offs of one group overlap the other's forward recompute.
+    const int gsz = GROUP == 2 ? (cw < 2 ? min(2, cmax) : cmax - 2) : 1;  // waves in this group
+    const int nbase = GROUP == 2 ? rcount * 6 * CW + (cw < 2 ? 0 : 6 * min(2, cmax)) + 2 * (cw & 1)
+                                 : rcount * 6 * CW + 6 * cw;
+    // (only a workgroup's last round can be partial)
     const int tile = rd * CW + cw;
     cbarrier();
     // per-tile lane id: nothing lane-derived (row addresses, LDS offsets) is hoisted out of the
@@ -480,7 +490,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       pin(a3);
       sched_fence();
       EB_STAMP(4);
-      produce_pair(lds, nbase + 0 * cmax + 2 * cw, op, a3, fresh_lane(lane), EB_IST(0));
+      produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
       EB_STAMP(5);
       gemm_cols(acc, op, lds + 3 * IMG_B, fresh_lane(lane));
       relu_select(A, acc, a3);
@@ -489,7 +499,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     op.set(A);  // G2
     pin(op);
-    produce_pair(lds, nbase + 2 * cmax + 2 * cw, op, a2, fresh_lane(lane), EB_IST(2));
+    produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
     relu_select(A, acc, a2);
@@ -513,7 +523,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
       }
     }
-    produce_pair(lds, nbase + 4 * cmax + 2 * cw, op, a1, fresh_lane(lane), EB_IST(4));
+    produce_pair(lds, nbase + 4 * gsz, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
     gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
     relu_select(A, acc, a1);
@@ -580,9 +590,11 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
 #endif
   for (int rd = rw.first; rd < rw.end; rd += rw.step) {
     const int cmax = min(CW, ntiles - rd * CW);
+    for (int grp = 0; grp < CW / GROUP; ++grp) {  // the chain waves' item order (chain_wave): group, layer, wave
+    const int gsz = GROUP == 2 ? (grp == 0 ? min(2, cmax) : max(0, cmax - 2)) : (grp < cmax ? 1 : 0);
 #pragma unroll
     for (int li = 0; li < 3; ++li) {  // 0: L = 3, 1: L = 2, 2: L = 1
-      for (int cc = 0; cc < cmax; ++cc, n += 2) {
+      for (int cc = 0; cc < gsz; ++cc, n += 2) {
         // a chain wave's pair (items n, n + 1: both halves of its tile) is taken at once: one
         // LDS round trip for its 16 reads instead of two
         const int k0 = n % NSLOT, j0 = n / NSLOT;
@@ -637,6 +649,7 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
           }
         }
       }
+    }
     }
   }
 #ifdef AGN_EB_STAMPS

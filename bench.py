@@ -491,6 +491,12 @@ def main():
             n, ms, by, fl, impl, has = kernels[tag]["_sum"]
             ach = basis_bytes / (ms * 1e-3) / 1e9
             traffic = (pmc or {}).get("per_launch_bytes", {}).get(tag)
+            disp = (pmc or {}).get("dispatch_bytes", {}).get(tag)
+            steps_pmc = (pmc or {}).get("steps")
+            if disp and steps_pmc:  # the tag's own launches: the largest n/step x steps dispatches
+                k = int(round(n / args.profile_steps)) * steps_pmc
+                if 0 < k <= len(disp):
+                    traffic = sum(sorted(disp)[-k:]) / k
             return {"kernel": tag, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "alg_bytes_per_launch": basis_bytes / n,

@@ -73,7 +73,7 @@ def main():
     for r in (1, 2):
         for li in range(3):
             for c in range(4):
-                n = 24 * r + 8 * li + 2 * c
+                n = 24 * r + (12 if c >= 2 else 0) + 4 * li + 2 * (c & 1)  # edge_bwd.hip item order
                 pe, pf, pg = chi[c, r - 1, 2 * li] - t0
                 det = dwi[:, n - 24:n - 22, 1] - t0
                 rel = dwi[:, n - 24:n - 22, 2] - t0
