@@ -3,7 +3,7 @@
 #   1. rocprofv3 --kernel-trace --stats of bench.py (C3)         -> gpurun_out/prof_$TAG
 #   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), kernel trace only -> gpurun_out/pmc_{fetch,write}_$TAG
 #   3. tools/pmc_traffic.py -> gpurun_out/pmc_traffic_$TAG.json (per launch and per step)
-#   4. the same two PMC passes with the fused edge backward (AEROGNN_FUSED_EDGE_BWD=1)
+#   4. the same two PMC passes on the split edge backward (AEROGNN_FUSED_EDGE_BWD=0)
 #   5. one MFMA-busy pass (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE) -> mfma_$TAG.json
 #   6. one stall pass (wave cycles split into waiting / issue-blocked / issuing) -> sq_$TAG.json
 #   7. the concat edge-MLP layer's kernel trace (no torch kernels) -> prof_concat_$TAG
@@ -23,12 +23,12 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/p
     python $B --steps 1 --warmup 1 > gpurun_out/pmc_write_$TAG.log 2>&1
 # 3 steps per PMC run: 1 warm-up, 1 timed, 1 instrumented (bench.py --profile-steps 1)
 python tools/pmc_traffic.py gpurun_out/pmc_fetch_$TAG gpurun_out/pmc_write_$TAG gpurun_out/pmc_traffic_$TAG.json 3
-AEROGNN_FUSED_EDGE_BWD=1 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-    -d gpurun_out/pmc_fetch_fused_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_fetch_fused_$TAG.log 2>&1
-AEROGNN_FUSED_EDGE_BWD=1 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-    -d gpurun_out/pmc_write_fused_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_write_fused_$TAG.log 2>&1
-python tools/pmc_traffic.py gpurun_out/pmc_fetch_fused_$TAG gpurun_out/pmc_write_fused_$TAG \
-    gpurun_out/pmc_traffic_fused_$TAG.json 3
+AEROGNN_FUSED_EDGE_BWD=0 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+    -d gpurun_out/pmc_fetch_split_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_fetch_split_$TAG.log 2>&1
+AEROGNN_FUSED_EDGE_BWD=0 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+    -d gpurun_out/pmc_write_split_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_write_split_$TAG.log 2>&1
+python tools/pmc_traffic.py gpurun_out/pmc_fetch_split_$TAG gpurun_out/pmc_write_split_$TAG \
+    gpurun_out/pmc_traffic_split_$TAG.json 3
 timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv \
     -d gpurun_out/pmc_mfma_$TAG -o c3 -- python $B --steps 1 --warmup 1 > gpurun_out/pmc_mfma_$TAG.log 2>&1
 python tools/mfma_busy.py gpurun_out/pmc_mfma_$TAG gpurun_out/mfma_$TAG.json
