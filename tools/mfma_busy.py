@@ -21,7 +21,7 @@ def main():
     acc = collections.defaultdict(lambda: collections.defaultdict(lambda: [0, 0.0]))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", r["Kernel_Name"].split("(")[0].replace("void ", ""))
+            name = re.sub(r"_ZN12_GLOBAL__N_1\d+", "", r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", ""))
             a = acc[name][r["Counter_Name"]]
             a[0] += 1
             a[1] += float(r["Counter_Value"])
