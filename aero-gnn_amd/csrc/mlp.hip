@@ -554,6 +554,12 @@ constexpr int RES_MAXL = 4;
 // live registers spill (measured: 2.55 -> 2.88 ms per launch with de staging), so both stay off
 constexpr bool kStageGradIn = false;
 constexpr bool kStageGradOut = false;
+#ifndef AGN_FWD_STAGE_IN
+#define AGN_FWD_STAGE_IN 1  // e tile loads through the LDS staging rows (1-KB instructions)
+#endif
+#ifndef AGN_FWD_STAGE_OUT
+#define AGN_FWD_STAGE_OUT 1  // e' stores through the LDS staging rows
+#endif
 #ifndef AGN_EARLY_E
 #define AGN_EARLY_E 0
 #endif
@@ -639,7 +645,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     BOp<T, NR> b;
     // kEarlyE: the e tile's loads go out before the projection rows are waited on (their
     // latencies overlap); off, the rows are gathered and summed first (two latencies per tile)
-    const bool staged_in = sg.ld == H;
+    const bool staged_in = AGN_FWD_STAGE_IN && sg.ld == H;
     uint4 eraw[NR / 8];
     if (kEarlyE && staged_in)
       tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32, lane);
@@ -731,7 +737,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * H : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
-    const bool stage_out = a.out_ld == H;
+    const bool stage_out = AGN_FWD_STAGE_OUT && a.out_ld == H;
     uint4 ob[NR / 8];  // e' row as 16-B chunks (chunk 2i+h of the row), for the staged store
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
