@@ -83,15 +83,33 @@ struct StageRegs {
       for (int j = 0; j < NCH; ++j) {
         const int i = threadIdx.x + j * DW_THREADS;
         const int r = i / CHUNKS, ch = i - r * CHUNKS;
-        const int gr = r0 + r;
-        const size_t sr = (gr < rows && idx) ? (size_t)idx[gr] : (size_t)gr;
-        T e8[PER16];
+        const int gr = r0 + r, gc0 = c0 + ch * PER16;
+        v[j] = uint4{0u, 0u, 0u, 0u};
+        // chunks past the last column stay zero without a load (a narrow X, e.g. K = 4, has one
+        // live chunk per row); a live chunk takes the widest aligned loads it can
+        if (gr < rows && gc0 < cols) {
+          const size_t sr = idx ? (size_t)idx[gr] : (size_t)gr;
+          const T* p = g + sr * ld + gc0;
+          const int nv = min(PER16, cols - gc0);
+          const uintptr_t pa = reinterpret_cast<uintptr_t>(p);
+          if (nv == PER16 && (pa & 15) == 0) {
+            v[j] = *reinterpret_cast<const uint4*>(p);
+          } else if (sizeof(T) == 2 && nv >= 4 && (pa & 7) == 0) {
+            typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 lo = *reinterpret_cast<const u32x2*>(p);
+            T e4[4] = {from_f<T>(0.f), from_f<T>(0.f), from_f<T>(0.f), from_f<T>(0.f)};
 #pragma unroll
-        for (int e = 0; e < PER16; ++e) {
-          const int gc = c0 + ch * PER16 + e;
-          e8[e] = (gr < rows && gc < cols) ? g[sr * ld + gc] : from_f<T>(0.f);
+            for (int e = 0; e < 4; ++e)
+              if (4 + e < nv) e4[e] = p[4 + e];
+            const u32x2 hi = *reinterpret_cast<const u32x2*>(e4);
+            v[j] = __builtin_bit_cast(uint4, u32x4{lo[0], lo[1], hi[0], hi[1]});
+          } else {
+            T e8[PER16];
+#pragma unroll
+            for (int e = 0; e < PER16; ++e) e8[e] = e < nv ? p[e] : from_f<T>(0.f);
+            v[j] = *reinterpret_cast<const uint4*>(e8);
+          }
         }
-        v[j] = *reinterpret_cast<const uint4*>(e8);
       }
     }
   }

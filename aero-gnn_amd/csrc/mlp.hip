@@ -558,7 +558,7 @@ constexpr bool kStageGradOut = false;
 #define AGN_FWD_STAGE_IN 1  // e tile loads through the LDS staging rows (1-KB instructions)
 #endif
 #ifndef AGN_FWD_STAGE_OUT
-#define AGN_FWD_STAGE_OUT 1  // e' stores through the LDS staging rows
+#define AGN_FWD_STAGE_OUT 0  // e' stores through the LDS staging rows (direct 16-B stores measured faster)
 #endif
 #ifndef AGN_EARLY_E
 #define AGN_EARLY_E 0
