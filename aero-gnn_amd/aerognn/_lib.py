@@ -37,7 +37,7 @@ class MlpFwdArgs(C.Structure):
                 ("proj", vp), ("src", vp), ("dst", vp),
                 ("resid", vp), ("out", vp),
                 ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32),
-                ("mask", vp * MAX_LIN)]
+                ("mask", vp * MAX_LIN), ("agg", vp), ("agg_mean", i32), ("_pad3", i32)]
 
 
 class MlpBwdArgs(C.Structure):
@@ -101,7 +101,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
-            "agn_proj_forward", "agn_proj_backward")
+            "agn_proj_forward", "agn_proj_backward", "agn_segment_sum_fixup")
 
 
 class AeroGNNError(RuntimeError):
@@ -155,6 +155,7 @@ def lib():
             "agn_packed_bytes": (C.c_size_t, [i32, i32, i32]),
             "agn_pack": (i32, [vp, i32, i32, vp]),
             "agn_mlp_forward": (i32, [C.POINTER(MlpFwdArgs), vp]),
+            "agn_mlp_fwd_agg_ok": (i32, [C.POINTER(MlpFwdArgs)]),
             "agn_mlp_bwd_nwaves": (i32, [i32]),
             "agn_mlp_backward": (i32, [C.POINTER(MlpBwdArgs), vp]),
             "agn_reduce_partials": (i32, [vp, i32, i32, vp, vp]),
@@ -164,6 +165,7 @@ def lib():
             "agn_wgrad_plan": (i32, [C.POINTER(WgradBatch)]),
             "agn_colsum": (i32, [vp, i32, i32, vp, i32, vp, vp]),
             "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
+            "agn_segment_sum_fixup": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp]),
             "agn_segment_sum2": (i32, [i32, i32, i32, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp]),
             "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
             "agn_segment_max": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, vp]),

@@ -196,8 +196,12 @@ class Pack:
 # ----------------------------------------------------------------------------- fused MLP chain
 def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out_ld=None,
                 ln=None, proj=None, src=None, dst=None, resid=None, acts=None, hpre=None, stats=None,
-                tag=None, cost=None):
-    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor)."""
+                tag=None, cost=None, agg=None, agg_mean=False):
+    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor).
+
+    agg: optional [*, out_dim] buffer for the receiver sums fused into the edge kernel
+    (agn_mlp_fwd_args.agg); returns True when the launch wrote them (resident edge kernel),
+    False when it did not (agg then untouched)."""
     a = L.MlpFwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
     a.out_dim, a.nseg = out_dim, len(segs)
@@ -218,8 +222,12 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
             a.mask[i] = ptr(_mask_of(t))
     a.hpre, a.stats = ptr(hpre), ptr(stats)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
+    fused_agg = False
+    if agg is not None and L.lib().agn_mlp_fwd_agg_ok(C.byref(a)):
+        a.agg, a.agg_mean, fused_agg = ptr(agg), int(agg_mean), True
     with timed(tag, cost):
         check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
+    return fused_agg
 
 
 # The persistent projection kernels (csrc/proj.hip) for the sum-trick edge block's node-row
@@ -325,6 +333,31 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
 
 def reduce_partials(partial, nw, n, out):
     check(L.lib().agn_reduce_partials(ptr(partial), nw, n, ptr(out), stream()), "reduce_partials")
+
+
+def edge_agg_fused() -> bool:
+    """Receiver aggregation of the node update (mgnLayer.py:144-146) fused into the resident edge
+    kernel (agn_mlp_fwd_args.agg) plus agn_segment_sum_fixup for receivers crossing a 32-edge tile,
+    instead of the node kernel's in-kernel walk over E rows (AEROGNN_EDGE_AGG=1; off by default).
+    Bitwise the same values either way; measured slower (session r3s): the
+    edge kernel's store drain + L2 re-read of each tile costs more than the node kernel saves."""
+    import os
+    return os.environ.get("AEROGNN_EDGE_AGG", "0") == "1"
+
+
+def segment_sum_fixup(rows, k, ptr_t, src, out, mean=False, tile=32):
+    check(L.lib().agn_segment_sum_fixup(rows, k, dt_code(src.dtype), ptr(ptr_t), ptr(src), src.stride(0), ptr(out),
+                                        out.stride(0), int(mean), tile, stream()), "segment_sum_fixup")
+    return out
+
+
+def node_presum() -> bool:
+    """Receiver aggregation of the MeshGraphNet node update (mgnLayer.py:144-146) as a separate
+    agn_segment_sum launch feeding the node kernel a PLAIN input (AEROGNN_NODE_PRESUM=1), instead
+    of the node kernel's in-kernel SUM / MEAN segment walk. Bitwise the same values either way;
+    measured no faster (the standalone walk costs what the node kernel saves)."""
+    import os
+    return os.environ.get("AEROGNN_NODE_PRESUM", "0") == "1"
 
 
 def segment_sum(rows, k, ptr_t, perm, src, out, mean=False, src_ld=None, out_ld=None):
