@@ -162,6 +162,52 @@ AGN_DEV void load_row_narrow(float (&v)[NR], const T* rowp, int k, int h) {
   }
 }
 
+// load_segment's SUM / MEAN walk with two member rows' loads in flight per step (adds in edge
+// order, one rounding: the same values). Run before anything else of the wave is live.
+#ifndef AGN_WALK2
+#define AGN_WALK2 1
+#endif
+template <int NR>
+AGN_DEV void walk2_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid, int h) {
+  const bf16* base = reinterpret_cast<const bf16*>(s.ptr);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) in[i] = 0.f;
+  const int beg = s.index[rr], end = s.index[rr + 1];
+  int j = beg;
+  for (; j + 1 < end; j += 2) {
+    uint4 r0[NR / 8], r1[NR / 8];
+    const bf16* p0 = base + (size_t)j * s.ld;
+    const bf16* p1 = p0 + s.ld;
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) r0[i] = *reinterpret_cast<const uint4*>(p0 + 16 * i + 8 * h);
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) r1[i] = *reinterpret_cast<const uint4*>(p1 + 16 * i + 8 * h);
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      float o[8];
+      unpack8_w(o, r0[i]);  // load8_w's exchange + conversion
+#pragma unroll
+      for (int e = 0; e < 8; ++e) in[8 * i + e] += o[e];
+    }
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      float o[8];
+      unpack8_w(o, r1[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) in[8 * i + e] += o[e];
+    }
+  }
+  if (j < end) add_row_w<bf16, NR>(in, base + (size_t)j * s.ld, h);
+  if (s.kind == AGN_SEG_MEAN) {
+    const float cnt = (float)max(end - beg, 1);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) in[i] = in[i] / cnt;
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) in[i] = round_t<bf16>(in[i]);
+  if (s.store) store_row<bf16, NR, true>(reinterpret_cast<bf16*>(s.store) + (size_t)rr * s.k, s.k, in, h, valid);
+}
+
 template <typename T, int NT, int MODE>
 __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
@@ -188,6 +234,18 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
   int k0 = 0;
   for (int s = 0; s < a.nseg; ++s) k0 += a.seg[s].k;
   const int ku0 = units_k<T>(k0);
+  // a node MLP's SUM / MEAN input is walked first, while nothing else of the wave is live, and
+  // kept packed until its GEMM (the layer-0 GEMM order, hence every sum, is unchanged)
+  constexpr bool W2 = AGN_WALK2 && MODE == M_VEC && std::is_same<T, bf16>::value && NT == 4;
+  const bool walk2 = W2 && a.nseg == 2 && (a.seg[1].kind == AGN_SEG_SUM || a.seg[1].kind == AGN_SEG_MEAN) &&
+                     a.seg[1].k == H;
+  BOp<T, NR> bagg;
+  if constexpr (W2) {
+    if (walk2) {
+      walk2_segment<NR>(v, a.seg[1], rr, valid, h);
+      bagg.set(v);
+    }
+  }
   const int ngrp = (a.nlin == 1) ? (a.out_dim + H - 1) / H : 1;
 
   for (int grp = 0; grp < ngrp; ++grp) {
@@ -239,9 +297,13 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
             staged = true;
           }
         }
-        if (!staged) load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
+        if (!staged) {
+          if (W2 && walk2 && s == 1) staged = true;
+          else load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
+        }
       }
-      b.set(v);
+      if (W2 && walk2 && s == 1) b = bagg;
+      else b.set(v);
       __syncthreads();
       if constexpr (IN_FULL) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
       else if constexpr (MODE == M_NIN) gemm<T, NT, NR, true>(acc, b, nu, wl, nu, NT, lane);
