@@ -37,7 +37,7 @@ class MlpFwdArgs(C.Structure):
                 ("proj", vp), ("src", vp), ("dst", vp),
                 ("resid", vp), ("out", vp),
                 ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32),
-                ("mask", vp * MAX_LIN), ("agg", vp), ("agg_mean", i32), ("_pad3", i32)]
+                ("mask", vp * MAX_LIN)]
 
 
 class MlpBwdArgs(C.Structure):
@@ -101,7 +101,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
-            "agn_proj_forward", "agn_proj_backward", "agn_segment_sum_fixup")
+            "agn_proj_forward", "agn_proj_backward")
 
 
 class AeroGNNError(RuntimeError):
@@ -155,7 +155,6 @@ def lib():
             "agn_packed_bytes": (C.c_size_t, [i32, i32, i32]),
             "agn_pack": (i32, [vp, i32, i32, vp]),
             "agn_mlp_forward": (i32, [C.POINTER(MlpFwdArgs), vp]),
-            "agn_mlp_fwd_agg_ok": (i32, [C.POINTER(MlpFwdArgs)]),
             "agn_mlp_bwd_nwaves": (i32, [i32]),
             "agn_mlp_backward": (i32, [C.POINTER(MlpBwdArgs), vp]),
             "agn_reduce_partials": (i32, [vp, i32, i32, vp, vp]),
@@ -165,7 +164,6 @@ def lib():
             "agn_wgrad_plan": (i32, [C.POINTER(WgradBatch)]),
             "agn_colsum": (i32, [vp, i32, i32, vp, i32, vp, vp]),
             "agn_segment_sum": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, i32, vp]),
-            "agn_segment_sum_fixup": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp]),
             "agn_segment_sum2": (i32, [i32, i32, i32, vp, i32, vp, vp, vp, i32, vp, vp, vp, i32, vp, i32, vp]),
             "agn_gather_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp]),
             "agn_segment_max": (i32, [i32, i32, i32, vp, vp, vp, i32, vp, i32, vp, vp]),
@@ -200,6 +198,7 @@ def lib():
             "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),
             "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
+            "agn_fault_status": (i32, [C.POINTER(i32), i32]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_proj_forward": (i32, [i32, vp, i32, vp, vp, vp, i32, vp]),
             "agn_proj_backward": (i32, [i32, vp, vp, i32, vp, vp, i32, vp]),
@@ -226,6 +225,14 @@ def check(rc: int, what: str = ""):
     if rc != 0:
         msg = lib().agn_error_string(rc).decode()
         raise AeroGNNError(f"aerognn {what} failed: {msg} (code {rc})")
+
+
+def fault_status(reset=True) -> int:
+    """The device fault word (include/aerognn.h agn_fault_status): nonzero if a bounded LDS-ring
+    wait of agn_edge_bwd_fused gave up since the last reset. Synchronises the device."""
+    v = i32(0)
+    check(lib().agn_fault_status(C.byref(v), 1 if reset else 0), "fault_status")
+    return int(v.value)
 
 
 def ptr(t):

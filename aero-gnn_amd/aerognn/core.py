@@ -196,12 +196,8 @@ class Pack:
 # ----------------------------------------------------------------------------- fused MLP chain
 def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out_ld=None,
                 ln=None, proj=None, src=None, dst=None, resid=None, acts=None, hpre=None, stats=None,
-                tag=None, cost=None, agg=None, agg_mean=False):
-    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor).
-
-    agg: optional [*, out_dim] buffer for the receiver sums fused into the edge kernel
-    (agn_mlp_fwd_args.agg); returns True when the launch wrote them (resident edge kernel),
-    False when it did not (agg then untouched)."""
+                tag=None, cost=None):
+    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor)."""
     a = L.MlpFwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
     a.out_dim, a.nseg = out_dim, len(segs)
@@ -222,12 +218,8 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
             a.mask[i] = ptr(_mask_of(t))
     a.hpre, a.stats = ptr(hpre), ptr(stats)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
-    fused_agg = False
-    if agg is not None and L.lib().agn_mlp_fwd_agg_ok(C.byref(a)):
-        a.agg, a.agg_mean, fused_agg = ptr(agg), int(agg_mean), True
     with timed(tag, cost):
         check(L.lib().agn_mlp_forward(C.byref(a), stream()), "mlp_forward")
-    return fused_agg
 
 
 # The persistent projection kernels (csrc/proj.hip) for the sum-trick edge block's node-row
@@ -284,6 +276,9 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
     return a.ln_rows
 
 
+# AEROGNN_CHECK_FAULTS=1 (set by the test suite): read the device fault word after every
+# persistent hand-off launch (a device synchronisation each time; never on the timed path).
+CHECK_FAULTS = __import__("os").environ.get("AEROGNN_CHECK_FAULTS", "0") == "1"
 STAMPS = None  # diagnostics: a uint64 device tensor of 2*8*8*16 entries (a -DAGN_EB_STAMPS library)
 
 
@@ -320,6 +315,10 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
     a.stamps = ptr(STAMPS)
     with timed(tag, cost):
         check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
+    if CHECK_FAULTS:  # tests / debug runs: a bounded ring wait that gave up is an error, not wrong dW
+        f = L.fault_status(reset=True)
+        if f:
+            raise L.AeroGNNError(f"agn_edge_bwd_fused: device fault word {f:#x} (LDS ring wait timed out; dW invalid)")
     dw = torch.empty(3, H, H, dtype=torch.float32, device=dev)
     db = torch.empty(3, H, dtype=torch.float32, device=dev)
     b = L.WgradBatch()
@@ -333,31 +332,6 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
 
 def reduce_partials(partial, nw, n, out):
     check(L.lib().agn_reduce_partials(ptr(partial), nw, n, ptr(out), stream()), "reduce_partials")
-
-
-def edge_agg_fused() -> bool:
-    """Receiver aggregation of the node update (mgnLayer.py:144-146) fused into the resident edge
-    kernel (agn_mlp_fwd_args.agg) plus agn_segment_sum_fixup for receivers crossing a 32-edge tile,
-    instead of the node kernel's in-kernel walk over E rows (AEROGNN_EDGE_AGG=1; off by default).
-    Bitwise the same values either way; measured slower (session r3s): the
-    edge kernel's store drain + L2 re-read of each tile costs more than the node kernel saves."""
-    import os
-    return os.environ.get("AEROGNN_EDGE_AGG", "0") == "1"
-
-
-def segment_sum_fixup(rows, k, ptr_t, src, out, mean=False, tile=32):
-    check(L.lib().agn_segment_sum_fixup(rows, k, dt_code(src.dtype), ptr(ptr_t), ptr(src), src.stride(0), ptr(out),
-                                        out.stride(0), int(mean), tile, stream()), "segment_sum_fixup")
-    return out
-
-
-def node_presum() -> bool:
-    """Receiver aggregation of the MeshGraphNet node update (mgnLayer.py:144-146) as a separate
-    agn_segment_sum launch feeding the node kernel a PLAIN input (AEROGNN_NODE_PRESUM=1), instead
-    of the node kernel's in-kernel SUM / MEAN segment walk. Bitwise the same values either way;
-    measured no faster (the standalone walk costs what the node kernel saves)."""
-    import os
-    return os.environ.get("AEROGNN_NODE_PRESUM", "0") == "1"
 
 
 def segment_sum(rows, k, ptr_t, perm, src, out, mean=False, src_ld=None, out_ld=None):

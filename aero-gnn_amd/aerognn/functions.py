@@ -21,7 +21,7 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
-from .core import (Pack, WGrad, node_presum, edge_agg_fused, segment_sum_fixup, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
+from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
                    cost_edge_bwd_fused,
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
@@ -244,6 +244,10 @@ class PermuteRowsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, perm32, inv32):
         require_device(x)
+        if x.dim() != 2 or x.shape[0] != perm32.numel() or perm32.numel() != inv32.numel():
+            # the gather kernel trusts its index: a row-count mismatch would read past the buffers
+            raise ValueError(f"edge rows: got a tensor of shape {tuple(x.shape)} for a level with "
+                             f"E = {perm32.numel()} edges (expected [E, features])")
         x = _c(x)
         ctx.inv32 = inv32
         return gather_rows(x.shape[0], x.shape[1], perm32, x, torch.empty_like(x))
@@ -398,19 +402,13 @@ class GMPFn(torch.autograd.Function):
                             segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
                             wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
                             tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
-            mean = spec.aggregation == "mean"
-            agg_buf = None
-            if edge_agg_fused() and not node_presum():
-                agg_buf = torch.empty(N, H, dtype=dt, device=dev)
-            fused_agg = mlp_forward(
-                        rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
-                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est, agg=agg_buf, agg_mean=mean,
+                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
                         tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
                                                                                             train and not fused)))
         else:
-            fused_agg = False
             se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
             ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
             sd = (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)
@@ -420,30 +418,19 @@ class GMPFn(torch.autograd.Function):
                         acts=ea, hpre=ehp, stats=est,
                         tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, x.element_size()),
                                                        cost_edge_fwd_cat(E, N, H, x.element_size(), es.nlin, train)))
+        # receiver aggregation (mgnLayer.py:144-146): the node kernel's SUM / MEAN input segment
+        # walks each receiver's CSC range in edge order (torch_scatter's fp32 order); in training it
+        # also stores the sums for the backward. (A separate segment-sum launch and sums fused into
+        # the edge kernel were measured slower: DESIGN.md §9, round 3.)
         kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
-        agg = torch.empty(N, H, dtype=dt, device=dev) if train and not fused_agg else None
-        if fused_agg:
-            # the edge kernel wrote the receivers inside one 32-edge tile; the rest (crossing a
-            # tile boundary, or without edges) in edge order here: the node kernel reads a PLAIN
-            # input, bitwise its own SUM / MEAN walk
-            agg = segment_sum_fixup(N, H, level.rowptr, e_out, agg_buf, mean=(kind == L.SEG_MEAN))
-            aseg = (L.SEG_PLAIN, H, agg.stride(0), agg, None, None)
-        elif node_presum():
-            # receiver sums in their own streaming launch (agn_segment_sum: fp32 in edge order,
-            # one rounding, bitwise the node kernel's in-kernel SUM / MEAN segment), then read as
-            # a PLAIN input: the node kernel's waves no longer walk E rows one lane at a time
-            if agg is None:
-                agg = torch.empty(N, H, dtype=dt, device=dev)
-            segment_sum(N, H, level.rowptr, None, e_out, agg, mean=(kind == L.SEG_MEAN))
-            aseg = (L.SEG_PLAIN, H, agg.stride(0), agg, None, None)
-        else:
-            aseg = (kind, H, e_out.stride(0), e_out, level.rowptr, agg)
+        agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
+        aseg = (kind, H, e_out.stride(0), e_out, level.rowptr, agg)
         mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None), aseg],
                     wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), resid=x, out=x_out,
                     acts=na, hpre=nhp, stats=nst,
                     tag="node_fwd", cost=with_alg(alg8d_node(N, H, x.element_size()),
-                                                   cost_node_fwd(N if fused_agg else E, N, H, x.element_size(),
+                                                   cost_node_fwd(E, N, H, x.element_size(),
                                                                  ns.nlin, train)))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)

@@ -137,11 +137,13 @@ def _gather_bwd(ctx, g):
     # d src[r] = sum over i with index[i] == r of g[i], divided by the caller's group size
     # max(rowptr[r+1] - rowptr[r], 1) when the forward divided by it (any rowptr, not only
     # group_ptr(index))
-    d = torch.ops.aerognn.scatter_sum(g, index, ctx.n, False)
-    if rowptr is not None:
-        cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).to(d.dtype)
-        d = d / cnt[:, None]
-    return d, None, None
+    if rowptr is None:
+        return torch.ops.aerognn.scatter_sum(g, index, ctx.n, False), None, None
+    # sum and divide in fp32 and round once, as the forward's in-kernel fp32 division does (a bf16
+    # count would round group sizes above 256, a bf16 sum would round before the division)
+    d = torch.ops.aerognn.scatter_sum(g.float(), index, ctx.n, False)
+    cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).to(torch.float32)
+    return (d / cnt[:, None]).to(g.dtype), None, None
 
 
 torch.library.register_autograd("aerognn::gather_rows", _gather_bwd, setup_context=_gather_ctx)

@@ -95,7 +95,13 @@ AGN_DEV void swap_halves(uint32_t& a, uint32_t& b) {
   a = r[0];
   b = r[1];
 }
-AGN_DEV uint32_t pack2(float x, float y) { return __builtin_bit_cast(uint32_t, bf16x2{(bf16)x, (bf16)y}); }
+// One v_cvt_pk_bf16_f32 per pair (RNE per element, the same rounding as two scalar casts). Built
+// with a vector convert: the scalar-cast form {(bf16)x, (bf16)y} lowers to two single-source
+// conversions plus a v_perm once the pair feeds integer ops (relu_pk16), 3 VALU instead of 1.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+AGN_DEV uint32_t pack2(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{x, y}, bf16x2));
+}
 AGN_DEV float lo_bf16(uint32_t u) { return __uint_as_float(u << 16); }
 AGN_DEV float hi_bf16(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 // the same for either 16-bit storage type (T = bf16 / f16; fp16 converts, bf16 shifts)
@@ -109,7 +115,9 @@ AGN_DEV uint32_t relu_pk16(uint32_t x) {
 }
 template <typename T> AGN_DEV uint32_t pack2t(float x, float y);
 template <> AGN_DEV uint32_t pack2t<bf16>(float x, float y) { return pack2(x, y); }
-template <> AGN_DEV uint32_t pack2t<f16>(float x, float y) { return __builtin_bit_cast(uint32_t, f16x2{(f16)x, (f16)y}); }
+template <> AGN_DEV uint32_t pack2t<f16>(float x, float y) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{x, y}, f16x2));
+}
 template <typename T> AGN_DEV float lo16(uint32_t u);
 template <typename T> AGN_DEV float hi16(uint32_t u);
 template <> AGN_DEV float lo16<bf16>(uint32_t u) { return lo_bf16(u); }
@@ -420,8 +428,8 @@ template <int NR> struct BOp<bf16, NR> {
   AGN_DEV void set(const float (&v)[NR]) {
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) u[i][j] = (bf16)v[8 * i + j];
+      u[i] = __builtin_bit_cast(bf16x8, u32x4{pack2(v[8 * i], v[8 * i + 1]), pack2(v[8 * i + 2], v[8 * i + 3]),
+                                              pack2(v[8 * i + 4], v[8 * i + 5]), pack2(v[8 * i + 6], v[8 * i + 7])});
   }
   AGN_DEV void mfma(f32x16& acc, const uint4& a_raw, int unit) const {
     bf16x8 a = *reinterpret_cast<const bf16x8*>(&a_raw);

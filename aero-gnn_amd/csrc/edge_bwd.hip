@@ -45,15 +45,9 @@ constexpr int NWAVE = 8;               // chain + dW waves
 constexpr int NTHR = 64 * NWAVE;
 constexpr int NSLOT = 3;
 #ifndef AGN_EB_GROUP
-#define AGN_EB_GROUP 2
+#define AGN_EB_GROUP 2  // chain waves per hand-off group (item order, chain_wave)
 #endif
 constexpr int GROUP = AGN_EB_GROUP;
-#ifndef AGN_EB_PFIRST
-#define AGN_EB_PFIRST 0  // issue the projection-row loads before g / dAgg at tile start
-#endif
-#ifndef AGN_EB_DEPTH
-#define AGN_EB_DEPTH 2  // weight-fragment prefetch depth of the row GEMMs
-#endif  // chain waves per hand-off group (item order, chain_wave)
 constexpr int IMG_B = H * H * 2;       // one 128 x 128 bf16 image (32 KB)
 constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
 constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
@@ -103,18 +97,6 @@ AGN_DEV void gemm_rows(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const char* im
     const int u = idx >> 2, ot = idx & 3;
     return *reinterpret_cast<const uint4*>((u & 1 ? po : pe) + 512 * (u >> 1) + 8192 * ot);
   };
-#if AGN_EB_DEPTH == 3
-  uint4 f0 = frag(0), f1 = frag(1), f2 = frag(2);
-#pragma unroll
-  for (int idx = 0; idx < 8 * NT; ++idx) {
-    const uint4 cur = f0;
-    f0 = f1;
-    f1 = f2;
-    if (idx + 3 < 8 * NT) f2 = frag(idx + 3);
-    b.mfma(acc[idx & 3], cur, idx >> 2);
-    __builtin_amdgcn_sched_barrier(0);  // keep the 3-deep prefetch: no hoisting of all 32 reads
-  }
-#else
   uint4 f0 = frag(0), f1 = frag(1);
 #pragma unroll
   for (int idx = 0; idx < 8 * NT; ++idx) {
@@ -124,7 +106,6 @@ AGN_DEV void gemm_rows(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const char* im
     b.mfma(acc[idx & 3], cur, idx >> 2);
     __builtin_amdgcn_sched_barrier(0);  // keep the 2-deep prefetch: no hoisting of all 32 reads
   }
-#endif
 }
 
 // acc[ot] = W^T[ot rows] . G^T (accumulators start at zero): A = W^T fragments by transposed reads of the same image. Lane
@@ -163,13 +144,21 @@ AGN_DEV void acc_bias(f32x16 (&acc)[NT], const float* pv, int h) {
   }
 }
 
-// Spin on an LDS counter. Bounded (about a second): a protocol error then yields wrong sums instead
-// of a wave that never finishes.
+// Spin on an LDS counter. Bounded (about half a second) so that a protocol error can never leave
+// a wave spinning forever; a wait that gives up is recorded in the device fault word (one lane,
+// a vector atomic OR), which agn_fault_status reports: the launch's dW / db are then wrong and
+// the caller must not use them.
+__device__ int g_agn_fault = 0;
 AGN_DEV void wait_ge(int* p, int v) {
+  bool ok = false;
   for (int spin = 0; spin < (1 << 24); ++spin) {
-    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) break;
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) {
+      ok = true;
+      break;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
+  if (!ok && __lane_id() == 0) __hip_atomic_fetch_or(&g_agn_fault, AGN_FAULT_RING_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("" ::: "memory");
 }
 // scheduling fence: keeps the machine scheduler from hoisting the next phase's LDS reads (bias,
@@ -316,19 +305,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
     const int sid = sid_next, did = did_next;
-#if AGN_EB_PFIRST
-    // the forward's projection rows go out first (their latency gates the first MFMA)
-    uint4 psr[NR / 8], pdr[NR / 8];
-    {
-      const bf16* ps = P + (size_t)sid * (2 * H);
-      const bf16* pd = P + (size_t)did * (2 * H) + H;
-#pragma unroll
-      for (int i = 0; i < NR / 8; ++i) {
-        psr[i] = *reinterpret_cast<const uint4*>(ps + 16 * i + 8 * h);
-        pdr[i] = *reinterpret_cast<const uint4*>(pd + 16 * i + 8 * h);
-      }
-    }
-#endif
     // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
     // forward recompute
     uint4 graw[NR / 8], g2raw[NR / 8];
@@ -349,16 +325,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     f32x16 acc[NT];
     BOp<bf16, NR> a1;  // the only activation kept from the forward pass
     {
-#if AGN_EB_PFIRST
-#pragma unroll
-      for (int i = 0; i < NR / 8; ++i) {
-        float x[8], y[8];
-        unpack8_w(x, psr[i]);  // load8_w's exchange + conversion
-        unpack8_w(y, pdr[i]);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
-      }
-#else
       const bf16* ps = P + (size_t)sid * (2 * H);
       const bf16* pd = P + (size_t)did * (2 * H) + H;
 #pragma unroll
@@ -369,7 +335,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
       }
-#endif
       BOp<bf16, NR> eop;
       float v[NR];
       load_row_w<bf16, NR>(v, reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
@@ -785,6 +750,17 @@ int agn_edge_bwd_blocks(int rows) {
   if (rounds >= g_cus) return g_cus;
   const int n = (rounds + 7) / 8 * 8;
   return n < 8 ? 8 : n;
+}
+
+int agn_fault_status(int* value, int reset) {
+  if (!value) return AGN_E_ARG;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(value, HIP_SYMBOL(g_agn_fault), sizeof(int));
+  if (e == hipSuccess && reset) {
+    const int zero = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_agn_fault), &zero, sizeof(int));
+  }
+  return e == hipSuccess ? 0 : (int)e;
 }
 
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {

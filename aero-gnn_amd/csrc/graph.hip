@@ -95,37 +95,6 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   }
 }
 
-// agn_segment_sum_fixup: segment_sum_kernel's value for the groups a fused receiver aggregation
-// left open (empty groups, groups spanning more than one `tile`-row tile); the others are skipped
-template <typename T>
-__global__ __launch_bounds__(256) void segment_sum_fixup_kernel(int rows, int k, const int32_t* __restrict__ ptr,
-                                                                const T* __restrict__ src, int src_ld,
-                                                                T* __restrict__ out, int out_ld, int mean, int tile) {
-  const int sub = threadIdx.x & (SEG_TPR - 1);
-  const int r = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
-  if (r >= rows) return;
-  const int beg = ptr[r], end = ptr[r + 1];
-  if (end > beg && beg / tile == (end - 1) / tile) return;  // written by the edge kernel
-  constexpr int A = 16 / sizeof(T);
-  const bool vec = ((k % A) == 0) && ((src_ld % A) == 0) && ((out_ld % A) == 0) &&
-                   ((((uintptr_t)src) | ((uintptr_t)out)) & 15) == 0;
-  for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int j = beg; j < end; ++j) {
-      float x[8];
-      load8(x, src + (size_t)j * src_ld, f0, k, vec);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] += x[i];
-    }
-    if (mean) {
-      const float cnt = (float)max(end - beg, 1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] /= cnt;
-    }
-    store8(out + (size_t)r * out_ld, f0, k, vec, s);
-  }
-}
-
 // out[r] = (base[r] + (group a of r)) + (group b of r): the concat edge MLP's node gradient in one
 // pass (agn_segment_sum2). Same thread layout and in-order fp32 accumulation as segment_sum_kernel.
 template <typename T>
@@ -712,23 +681,6 @@ int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_
   if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_F16) return seg_sum_t<f16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   return AGN_E_DTYPE;
-}
-
-int agn_segment_sum_fixup(int rows, int k, int dtype, const int32_t* ptr, const void* src, int src_ld, void* out,
-                          int out_ld, int mean, int tile, void* stream) {
-  if (rows < 0 || k < 1 || tile < 1 || !ptr || !out) return AGN_E_ARG;
-  if (rows == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  const dim3 g((rows + 15) / 16), b(256);
-#define AGN_SSF(T)                                                                                     \
-  hipLaunchKernelGGL(segment_sum_fixup_kernel<T>, g, b, 0, st, rows, k, ptr, (const T*)src, src_ld, (T*)out, \
-                     out_ld, mean, tile)
-  if (dtype == AGN_F32) AGN_SSF(float);
-  else if (dtype == AGN_BF16) AGN_SSF(bf16);
-  else if (dtype == AGN_F16) AGN_SSF(f16);
-  else return AGN_E_DTYPE;
-#undef AGN_SSF
-  return launch_status();
 }
 
 int agn_segment_sum2(int rows, int k, int dtype, const void* base, int base_ld, const int32_t* ptr_a,

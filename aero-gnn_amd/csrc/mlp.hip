@@ -616,16 +616,6 @@ constexpr int RES_MAXL = 4;
 // live registers spill (measured: 2.55 -> 2.88 ms per launch with de staging), so both stay off
 constexpr bool kStageGradIn = false;
 constexpr bool kStageGradOut = false;
-#ifndef AGN_FWD_STAGE_IN
-#define AGN_FWD_STAGE_IN 1  // e tile loads through the LDS staging rows (1-KB instructions)
-#endif
-#ifndef AGN_FWD_STAGE_OUT
-#define AGN_FWD_STAGE_OUT 0  // e' stores through the LDS staging rows (direct 16-B stores measured faster)
-#endif
-#ifndef AGN_EARLY_E
-#define AGN_EARLY_E 0
-#endif
-constexpr bool kEarlyE = AGN_EARLY_E;
 
 template <typename T, int NT>
 constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) * 64; }
@@ -666,61 +656,7 @@ __device__ unsigned long long* agn_fwd_stamps;
   } while (0)
 #endif
 
-// Receiver sums of one 32-row output tile (NodeBlock's scatter_add / scatter_mean of e',
-// mgnLayer.py:144-146, fused into the edge kernel): the wave re-reads the tile's stored e' rows
-// from L2 (lane l: features 2l, 2l+1 of every row; agent-scope loads, after the wave's stores have
-// drained) and walks them in row order, the receiver id uniform per row. A receiver whose whole
-// CSC range lies in this tile gets agg[dst] = fp32 sum (mean) of the stored values in row order,
-// one rounding: the node kernel's SUM / MEAN segment bit for bit. Receivers crossing a tile
-// boundary are left to agn_segment_sum_fixup.
-template <typename T>
-AGN_DEV void edge_tile_agg(const agn_mlp_fwd_args& a, int tile, int tdst, int lane) {
-  const int t0 = tile * 32;
-  const int nrow = min(32, a.rows - t0);
-  const int prev = t0 > 0 ? a.dst[t0 - 1] : -1;
-  const int next = t0 + 32 < a.rows ? a.dst[t0 + 32] : -1;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t* base = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(reinterpret_cast<const T*>(a.out) +
-                                                                            (size_t)t0 * a.out_ld)) + lane;
-  const int ldw = a.out_ld / 2;
-  uint32_t w[32];
-#pragma unroll
-  for (int r = 0; r < 32; ++r)
-    w[r] = r < nrow ? __hip_atomic_load(base + (size_t)r * ldw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-  uint32_t* ag = reinterpret_cast<uint32_t*>(a.agg) + lane;
-  // run starts / ends of the tile's rows as 32-bit masks (row c = lane c): a run is this tile's
-  // when a start bit lies at or below its end bit (else it began in the previous tile)
-  const int c = lane & 31;
-  const int dm1 = __shfl(tdst, (c + 31) & 31, 32), dp1 = __shfl(tdst, (c + 1) & 31, 32);
-  const bool vr = c < nrow;
-  const uint32_t smask = (uint32_t)__ballot(vr && tdst != (c == 0 ? prev : dm1));
-  const uint32_t emask = (uint32_t)__ballot(vr && tdst != (c == nrow - 1 ? next : dp1));
-  float s0 = 0.f, s1 = 0.f;
-#pragma unroll
-  for (int r = 0; r < 32; ++r) {
-    if ((smask >> r) & 1u) {
-      s0 = 0.f;
-      s1 = 0.f;
-    }
-    s0 += lo16<T>(w[r]);
-    s1 += hi16<T>(w[r]);
-    if ((emask >> r) & 1u) {
-      const uint32_t below = smask & (r == 31 ? 0xffffffffu : ((2u << r) - 1u));
-      if (below) {
-        const int d = __builtin_amdgcn_readlane(tdst, r);
-        float v0 = s0, v1 = s1;
-        if (a.agg_mean) {
-          const float cnt = (float)(r - (31 - __builtin_clz(below)) + 1);
-          v0 = v0 / cnt;
-          v1 = v1 / cnt;
-        }
-        ag[(size_t)d * (a.out_ld / 2)] = pack2t<T>(v0, v1);
-      }
-    }
-  }
-}
-
-template <typename T, int NT, bool AGG>
+template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
@@ -728,7 +664,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
-  __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e' stores
+  __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e loads
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
@@ -759,13 +695,10 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     const int rr = valid ? row : a.rows - 1;
     f32x16 acc[NT];
     BOp<T, NR> b;
-    // kEarlyE: the e tile's loads go out before the projection rows are waited on (their
-    // latencies overlap); off, the rows are gathered and summed first (two latencies per tile)
-    const bool staged_in = AGN_FWD_STAGE_IN && sg.ld == H;
+    // the projection rows are gathered and summed first, then the e tile goes through the staging
+    // rows (issuing the e loads ahead of the gathers measured slower: DESIGN.md §9, round 3)
+    const bool staged_in = sg.ld == H;
     uint4 eraw[NR / 8];
-    const int tdst = ndst;  // receiver of row c of this tile (agg walk)
-    if (kEarlyE && staged_in)
-      tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32, lane);
     if (a.proj) {
       const int cs = nsrc, cd = ndst;
       if (tile + tw.step < tw.end) {
@@ -791,9 +724,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     {
       float v[NR];
       if (staged_in) {  // coalesced 1-KB loads through the wave's LDS staging rows
-        if (!kEarlyE)
-          tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
-                                 lane);
+        tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
+                               lane);
         uint4 mine[NR / 8];
         tile_load_finish<H / 8>(mine, eraw, stg[threadIdx.x >> 6], lane);
 #pragma unroll
@@ -854,8 +786,6 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     T* hp = a.hpre ? reinterpret_cast<T*>(a.hpre) + (size_t)row * H : nullptr;
     const T* rp = a.resid ? reinterpret_cast<const T*>(a.resid) + (size_t)rr * a.out_ld : nullptr;
     T* op = reinterpret_cast<T*>(a.out) + (size_t)row * a.out_ld;
-    const bool stage_out = AGN_FWD_STAGE_OUT && a.out_ld == H;
-    uint4 ob[NR / 8];  // e' row as 16-B chunks (chunk 2i+h of the row), for the staged store
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
       float v[8];
@@ -882,16 +812,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = round_t<T>(v[e]) + r[e];
       }
-      if (stage_out) ob[i] = pack8_w(v, h);
-      else store8_w(op, i, h, v, valid);
+      store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
     }
     FWD_STAMP(11);
-    if (stage_out)  // 8-row passes through LDS: every store instruction writes 1 KB contiguous
-      tile_store_chunks<H / 8>(ob, reinterpret_cast<T*>(a.out) + (size_t)tile * 32 * H, a.rows - tile * 32,
-                               stg[threadIdx.x >> 6], lane);
-    FWD_STAMP(12);
-    if constexpr (AGG) edge_tile_agg<T>(a, tile, tdst, lane);  // its own instantiation: the default
-                                                               // kernel carries none of its registers
 #ifdef AGN_FWD_STAMPS
     ++ntile;
 #endif
@@ -1325,13 +1248,6 @@ int agn_mlp_bwd_nwaves(int rows) {
   return (waves + WPB - 1) / WPB;
 }
 
-int agn_mlp_fwd_agg_ok(const agn_mlp_fwd_args* a) {
-  if (!a || a->nseg != 1 || !a->proj || !a->dst) return 0;
-  const bool out_full = (a->out_ld % 8 == 0) && (a->nlin == 1 ? (a->out_dim % a->hidden == 0) : (a->out_dim == a->hidden));
-  const bool in_full = a->seg[0].k == a->hidden && a->seg[0].ld % 8 == 0;
-  return (in_full && out_full && fwd_ptrs_aligned(a) && res_fwd_ok(a, true)) ? 1 : 0;
-}
-
 int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   if (!a || a->rows < 0 || a->nlin < 1 || a->nlin > AGN_MAX_LIN || a->nseg < 1 || a->nseg > AGN_MAX_SEG)
     return AGN_E_ARG;
@@ -1357,11 +1273,9 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
     else if (in_full && a->nlin > 1 && a->out_dim <= 32 && !a->use_ln) mode = M_NOUT;
   }
   const bool vec = mode == M_VEC;
-  if (a->agg && !(res_fwd_ok(a, vec) && a->proj && a->dst)) return AGN_E_ARG;
   if (res_fwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
-    if (a->agg) hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4, true>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
-    else hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4, false>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
     return launch_status();
   }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));

@@ -40,9 +40,6 @@ struct Tiles {
   }
 };
 
-#ifndef PJ_STAGE_OUT
-#define PJ_STAGE_OUT 1  // output rows through the LDS staging rows (1-KB store instructions)
-#endif
 
 // NSEG input segments of 128 features; NGRP output groups of 128 (packed matrix: NGRP * 4 out
 // tiles x NSEG * 8 k-units, unit = (ot * KU + ku) * 64 + lane)
@@ -110,11 +107,11 @@ __global__ __launch_bounds__(PJ_BLOCK, 2) void proj_kernel(int rows, const bf16*
 #pragma unroll
           for (int e = 0; e < 8; ++e) v8[e] = round_t<bf16>(v8[e]) + r8[e];
         }
-        if (PJ_STAGE_OUT) ob[i] = pack8_w(v8, h);
-        else store8_w(out + (size_t)(tile * 32 + c) * out_ld + grp * H, i, h, v8, tile * 32 + c < rows);
+        ob[i] = pack8_w(v8, h);
       }
-      if (PJ_STAGE_OUT)
-        tile_store_chunks<H / 8>(ob, out + (size_t)tile * 32 * out_ld + grp * H, rows - tile * 32, stg[wid], lane,
+      // output rows through the LDS staging rows: 1-KB store instructions (direct 16-B stores
+      // measured slower, 94 -> 120 us per C3 launch: DESIGN.md §9, round 3)
+      tile_store_chunks<H / 8>(ob, out + (size_t)tile * 32 * out_ld + grp * H, rows - tile * 32, stg[wid], lane,
                                  out_ld / 8);
     }
   }

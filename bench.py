@@ -9,7 +9,8 @@ build, as the reference does) + MSE + backward + gradient all-reduce + Adam.
 An edge-update is one directed edge processed by one MeshGraphNetLayer (SURVEY §8d);
 EU/step is counted from the actual hierarchy.
 
-N GPUs (torchrun): every rank trains on its own mesh of the same size (rotation seed = rank),
+N GPUs: `bench.py --gpus N` starts N worker processes itself (one per GPU; or run it under
+torchrun with N ranks, whose WORLD_SIZE must equal --gpus): every rank trains on its own mesh of the same size (rotation seed = rank),
 one RCCL gradient all-reduce per step (bucketed, overlapped with the backward): weak scaling,
 value = total EU / max-rank time. The same run also measures the north-star scaling case,
 C4 strong scaling (BASELINE.json configs[3]: a fixed global batch of 64 ellipsoid(400,250)
@@ -316,6 +317,56 @@ def kernel_table(prof, steps, elapsed_step_s):
     return tab
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n, port, base=None):
+    """The environment of each of n worker ranks on this node (torchrun's variables, rendezvous on
+    127.0.0.1): rank r drives GPU r (LOCAL_RANK), HSA_ENABLE_IPC_MODE_LEGACY=0 kept (dmabuf IPC)."""
+    base = dict(os.environ if base is None else base)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started without torchrun: start N fresh worker processes of this script
+    (one per GPU, each a child process — nothing here has touched the GPU, and no exec), wait for
+    all of them and return the worst exit status. Rank 0 prints the JSON line. If a rank fails,
+    the others (the exact processes started here) are terminated so no rank waits forever in a
+    collective."""
+    import subprocess
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env)
+             for env in rank_envs(n, port)]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0:
+                    rc = rc or r
+                    for q in pending:
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -336,6 +387,14 @@ def main():
     if args.cpu_plan:
         print(json.dumps(cpu_plan()))
         return
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU, started here (the same run torchrun would make)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')} "
+                         f"(the launcher's rank count must equal --gpus)")
 
     from aerognn import core, dist as D
     rank, ws = D.init_from_env()

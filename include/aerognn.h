@@ -81,14 +81,6 @@ typedef struct {
   int tiled;                       /* 1: act/hpre in the tiled layout (AGN_TILED below, hidden-wide) */
   int _pad2;
   void* mask[AGN_MAX_LIN];         /* optional AGN_RELU_MASK of act[l] (may be given without act[l]) */
-  /* optional receiver aggregation of the output rows (mgnLayer.py:144-146), rows grouped by dst
-   * (CSC): agg[dst] = sum (agg_mean: mean) of the stored output rows of each receiver whose whole
-   * row range lies in one 32-row tile, fp32 in row order, one rounding. Receivers crossing a tile
-   * boundary and receivers without rows are left to agn_segment_sum_fixup. Needs the resident
-   * edge kernel (agn_mlp_fwd_agg_ok) and dst. */
-  void* agg;
-  int agg_mean;
-  int _pad3;
 } agn_mlp_fwd_args;
 
 typedef struct {
@@ -204,9 +196,6 @@ size_t agn_packed_bytes(int m, int k, int dtype);
 int agn_pack(const agn_pack_desc* descs_device, int n, int max_threads, void* stream);
 
 int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream);
-/* 1 if agn_mlp_forward runs these arguments on the resident edge kernel, the one that honours
- * agg (mgnLayer.py:93-105 + :144-146 fused); 0 otherwise (agg must then be NULL). */
-int agn_mlp_fwd_agg_ok(const agn_mlp_fwd_args* a);
 /* rows of ln_partial written by agn_mlp_backward (one per 256-row block) */
 int agn_mlp_bwd_nwaves(int rows);
 int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream);
@@ -216,11 +205,6 @@ int agn_reduce_partials(const float* partial, int nw, int n, float* out, void* s
 /* out[r] = sum (or mean) of src[perm ? perm[j] : j] for j in ptr[r]..ptr[r+1]-1; [rows][k] */
 int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_t* perm,
                     const void* src, int src_ld, void* out, int out_ld, int mean, void* stream);
-/* Completion of a fused receiver aggregation (agn_mlp_fwd_args.agg): out[r] = agn_segment_sum's
- * value for every group r that is empty or whose rows ptr[r]..ptr[r+1]-1 span more than one
- * `tile`-row tile; groups inside one tile are left untouched (the edge kernel wrote them). */
-int agn_segment_sum_fixup(int rows, int k, int dtype, const int32_t* ptr, const void* src, int src_ld,
-                          void* out, int out_ld, int mean, int tile, void* stream);
 /* out[r] = (base[r] + A[r]) + B[r], A[r] = sum_{j in ptr_a[r]..} src_a[perm_a ? perm_a[j] : j] and
  * B[r] likewise, each group summed from zero in index order, fp32, one rounding: the concat edge
  * MLP's node gradient dx + scatter_add(d x_src, src) + scatter_add(d x_dst, dst)
@@ -390,6 +374,11 @@ typedef struct {
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
+/* Device fault word of the persistent hand-off kernels (agn_edge_bwd_fused's LDS ring): the OR of
+ * AGN_FAULT_* bits recorded since the last reset (0 = none). A set bit means a bounded wait gave
+ * up and that launch's dW / db are wrong. Synchronises the device; reset != 0 clears the word. */
+#define AGN_FAULT_RING_TIMEOUT 1
+int agn_fault_status(int* value, int reset);
 /* dw[m][k] = sum_s dw_partial[s][m][k] (and db) for each desc: the fixed-order second stage
  * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);

@@ -8,6 +8,8 @@ PKG = os.path.join(ROOT, "aero-gnn_amd")
 for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
+# every persistent hand-off launch checks the device fault word in the test suite (aerognn.core)
+os.environ.setdefault("AEROGNN_CHECK_FAULTS", "1")
 
 
 def pytest_configure(config):

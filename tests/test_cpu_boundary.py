@@ -31,7 +31,7 @@ def test_struct_layouts_match_c(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     fields = {"agn_seg": (L.Seg, ["kind", "k", "ld", "ptr", "index", "store"]),
               "agn_pack_desc": (L.PackDesc, ["src", "dst", "rows", "trans", "row_off", "dst_cols"]),
-              "agn_mlp_fwd_args": (L.MlpFwdArgs, ["seg", "wpk", "bias", "ln_g", "proj", "resid", "act", "stats", "mask", "agg", "agg_mean"]),
+              "agn_mlp_fwd_args": (L.MlpFwdArgs, ["seg", "wpk", "bias", "ln_g", "proj", "resid", "act", "stats", "mask"]),
               "agn_mlp_bwd_args": (L.MlpBwdArgs, ["wtpk", "act", "g", "gidx", "gpre", "din_nseg", "din_k", "din",
                                                  "din_resid", "ln_partial"]),
               "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db", "nsplit", "xidx"]),

@@ -142,3 +142,22 @@ def test_forced_world_of_one_runs_collective_path(tmp_path):
     mp.start_processes(_forced_one_worker, args=(_free_port(), out), nprocs=1, join=True, start_method="spawn")
     r = torch.load(out, weights_only=True)
     assert r["ok"] and r["buckets"] >= 2 and r["fired"] == r["buckets"], r
+
+
+def test_bench_rank_envs_and_world_size_check():
+    """bench.py --gpus N without torchrun starts N ranks itself (bench.launch_ranks): each rank gets
+    torchrun's variables with a 127.0.0.1 rendezvous; under a launcher WORLD_SIZE must equal --gpus
+    (checked before anything touches a GPU)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    envs = bench.rank_envs(4, 29999, base={"PATH": "/usr/bin"})
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29999"
+               and e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" for e in envs)
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr, r.stderr[-2000:]

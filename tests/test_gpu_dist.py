@@ -108,6 +108,28 @@ def test_bench_two_ranks_json():
     assert d["config"]["parallelism"] == "dp2"
 
 
+def test_bench_self_launch_two_ranks_json():
+    """Plain `python bench.py --gpus 2` (no torchrun): bench starts its two ranks itself."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", AEROGNN_DIST_BACKEND="gloo", AEROGNN_MEMLOG="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--config", "small", "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the only line
+    d = json.loads(lines[0])
+    print(d["value"], d["collective"])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "dp2"
+    assert d["collective"]["world_size"] == 2 and d["collective"]["backend"] == "gloo"
+    assert d["config"]["edge_updates_per_step_all_ranks"] > d["config"]["edge_updates_per_step_per_gpu"]
+
+
+def test_bench_rejects_world_size_mismatch():
+    r = _torchrun(["bench.py", "--gpus", "2", "--config", "small", "--steps", "1", "--warmup", "0",
+                   "--no-cpu-baseline"], timeout=300, nproc=1)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr, r.stderr[-2000:]
+
+
 RCCL_WORKER = r'''
 import os, sys, json
 sys.path[:0] = [{root!r}, os.path.join({root!r}, "aero-gnn_amd")]

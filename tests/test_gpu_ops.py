@@ -48,6 +48,24 @@ def test_gather_rows_and_backward():
     assert torch.equal(s.grad.cpu(), torch.zeros_like(src).index_add_(0, idx, w))
 
 
+def test_gather_rows_mean_backward_bf16_large_groups():
+    """gather_rows with a group-size divisor (the broadcast side of a mean pool): its backward sums
+    and divides in fp32 and rounds once, so a 100,000-row group's gradient is the fp32 value rounded
+    to bf16 (a bf16 count would read 99,840)."""
+    import aerognn.ops  # noqa: F401
+    n, k = 100_000, 8
+    idx = torch.zeros(n, dtype=torch.long)
+    idx[60_000:] = 1
+    rowptr = torch.tensor([0, 60_000, n])
+    w = torch.randn(n, k, generator=torch.Generator().manual_seed(3)).bfloat16()
+    s = torch.zeros(2, k, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    (torch.ops.aerognn.gather_rows(s, idx.to(DEV), rowptr.to(DEV)).float() * w.to(DEV).float()).sum().backward()
+    ref = torch.zeros(2, k).index_add_(0, idx, w.float()) / torch.tensor([60_000.0, 40_000.0])[:, None]
+    got = s.grad.cpu().float()
+    print("max rel err", float(((got - ref).abs() / ref.abs()).max()))
+    assert torch.equal(s.grad.cpu(), ref.bfloat16()) or float(((got - ref).abs() / ref.abs()).max()) <= 2 ** -8
+
+
 @pytest.mark.parametrize("mean", [False, True])
 def test_scatter_sum_backward(mean):
     import aerognn.ops  # noqa: F401
