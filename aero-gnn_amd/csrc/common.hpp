@@ -448,6 +448,27 @@ template <int NR> struct BOp<bf16, NR> {
       u[i] = __builtin_bit_cast(bf16x8, w);
     }
   }
+  // From a row's 16-B chunks as loaded (chunk i of lane half h = features 16i+8h..+7) or as the
+  // staging rows hand them over ("exchanged": tile_load_finish): the lane-half swap of load8_w /
+  // unpack8_w puts the acc-order pairs in place, so the operand is the swapped dwords themselves,
+  // not an unpack to fp32 and a repack (identical bits: bf16 -> fp32 -> bf16 is exact; only a
+  // signalling NaN would come back quieted by the repack, which this path skips).
+  AGN_DEV void set_w(const uint4 (&mine)[NR / 8]) {
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      const u32x4 x = __builtin_bit_cast(u32x4, mine[i]);
+      uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+      swap_halves(a0, b0);
+      swap_halves(a1, b1);
+      u[i] = __builtin_bit_cast(bf16x8, u32x4{a0, a1, b0, b1});
+    }
+  }
+  AGN_DEV void load_w(const bf16* rowp, int h) {
+    uint4 raw[NR / 8];
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) raw[i] = *reinterpret_cast<const uint4*>(rowp + 16 * i + 8 * h);
+    set_w(raw);
+  }
   // registers 8i..8i+7 (acc order) as floats
   AGN_DEV void get8(float (&o)[8], int i) const {
 #pragma unroll
@@ -684,6 +705,13 @@ template <int M> AGN_DEV float partner(float v) {
   }
 }
 AGN_DEV float xor32(float v) { return partner<32>(v); }
+// v + (the value lane l ^ 32 holds): one v_permlane32_swap of v with itself leaves the lower half's
+// value in r[0] and the upper half's in r[1] on every lane, so the sum needs no lane select
+// (and a + b == b + a: bitwise v + xor32(v) on both halves)
+AGN_DEV float sum32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 // Transpose-reduce NR per-lane values over the 32 lanes of each half (lanes c = l & 31).
 // On return lane c holds in v[i] (i < max(NR/32,1)) the 32-lane sum of register
@@ -695,12 +723,23 @@ struct Butterfly {
     if constexpr (M >= 1) {
       if constexpr (N >= 2) {
         constexpr int HALF = N / 2;
-        const bool upper = (c & M) != 0;
+        if constexpr (M == 16) {
+          // v_permlane16_swap(x = v[i], y = v[HALF + i]) leaves (x_lo, x_up) on the lower row's
+          // lanes and (y_lo, y_up) on the upper row's: each row's keep + partner sum, no selects
 #pragma unroll
-        for (int i = 0; i < HALF; ++i) {
-          const float keep = upper ? v[HALF + i] : v[i];
-          const float send = upper ? v[i] : v[HALF + i];
-          v[i] = keep + partner<M>(send);
+          for (int i = 0; i < HALF; ++i) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[HALF + i]),
+                                                            false, false);
+            v[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+          }
+        } else {
+          const bool upper = (c & M) != 0;
+#pragma unroll
+          for (int i = 0; i < HALF; ++i) {
+            const float keep = upper ? v[HALF + i] : v[i];
+            const float send = upper ? v[i] : v[HALF + i];
+            v[i] = keep + partner<M>(send);
+          }
         }
         Butterfly<NR, HALF, M / 2>::run(v, c);
       } else {

@@ -236,10 +236,26 @@ AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<b
 #endif
 }
 
-// G_{L-1} = dA . [a_L > 0] (the split path's AGN_RELU_MASK select, from the packed activation)
-AGN_DEV void relu_select(float (&A)[NR], const f32x16 (&acc)[NT], const BOp<bf16, NR>& act) {
+// G_{L-1} = dA . [a_L > 0] (the split path's AGN_RELU_MASK select), packed: each pair of dA is
+// rounded to bf16 by one v_cvt_pk and ANDed with a 16-bit mask per half built from the packed
+// activation (relu outputs are +0 or positive int16 patterns: 0 - a is negative exactly when a > 0,
+// and its arithmetic shift by 15 is 0xffff or 0). Bitwise the select-then-round of the split path:
+// a dropped element is 0x0000 either way, a kept one is the same rounding of dA.
+typedef short s16x2v __attribute__((ext_vector_type(2)));
+AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const BOp<bf16, NR>& act) {
 #pragma unroll
-  for (int i = 0; i < NR; ++i) A[i] = bop_pos<NR>(act, i) ? acc[i / 16][i % 16] : 0.f;
+  for (int i = 0; i < NR / 8; ++i) {
+    const u32x4 a = __builtin_bit_cast(u32x4, act.u[i]);
+    u32x4 w;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = 8 * i + 2 * k;
+      const uint32_t p = pack2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]);
+      const s16x2v neg = s16x2v{0, 0} - __builtin_bit_cast(s16x2v, a[k]);
+      w[k] = p & __builtin_bit_cast(uint32_t, neg >> s16x2v{15, 15});
+    }
+    out.u[i] = __builtin_bit_cast(bf16x8, w);
+  }
 }
 
 // Diagnostic phase clocks (built with -DAGN_EB_STAMPS into a separate library; the product build
@@ -284,6 +300,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   };
   int sid_next = 0, did_next = 0;
   if (rw.first < rw.end) tile_ids(rw.first, sid_next, did_next);
+
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
     if (cw >= cmax) continue;
@@ -336,9 +353,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
       }
       BOp<bf16, NR> eop;
-      float v[NR];
-      load_row_w<bf16, NR>(v, reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
-      eop.set(v);
+      eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
       EB_STAMP(1);
       gemm_rows(acc, eop, lds + 0 * IMG_B, fresh_lane(lane));
     }
@@ -373,7 +388,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
-      s += xor32(s);
+      s = sum32(s);
       mean = s / (float)H;
       float q = 0.f;
 #pragma unroll
@@ -381,7 +396,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         const float d = acc[i / 16][i % 16] - mean;
         q = ln_sq_acc(q, d);
       }
-      q += xor32(q);
+      q = sum32(q);
       rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
     }
     // the pre-LN row as the split path stores it (bf16, acc order)
@@ -412,11 +427,14 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     // chunks: the butterfly's XOR order 16, 8, 4, 2, 1 gives each feature the same sums)
     {
       const float* gmv = pv + 3 * H;
+      // this wave's LayerNorm parameter partials: lane c adds sum g * xhat (c < 16) or sum g
+      // (c >= 16) of register 16 kk + (c & 15)
+      float* lnp = reinterpret_cast<float*>(lds + OFF_LNP) + cw * 2 * H + (c >> 4) * H;
       float c1 = 0.f, c2 = 0.f;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         sched_fence();
-        float B[16];
+        float B[32];  // [0, 16): g * xhat of registers 16 kk.., [16, 32): g of the same registers
 #pragma unroll
         for (int i = 2 * kk; i < 2 * kk + 2; ++i) {
           float hv[8];
@@ -433,19 +451,20 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
             }
           }
         }
-        // lane c holds the 32-row sums of register 16 kk + c/2 (pairs c, c^1 identical)
-        float* lp = reinterpret_cast<float*>(lds + OFF_LNP) + cw * 2 * H + feat_of(16 * kk + (c >> 1), h);
-        butterfly_reduce<16>(B, lane);
-        if ((c & 1) == 0) lp[0] += B[0];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) B[i] = A[16 * kk + i];
-        butterfly_reduce<16>(B, lane);
-        if ((c & 1) == 0) lp[H] += B[0];
+        for (int i = 0; i < 16; ++i) B[16 + i] = A[16 * kk + i];
+        // lane c holds the 32-row sum of B[c]: sum g * xhat (c < 16) or sum g (c >= 16) of register
+        // 16 kk + (c & 15); each feature's rows are added in the butterfly's XOR order 16, 8, 4, 2, 1
+        butterfly_reduce<32>(B, lane);
+        // running sum over the wave's tiles in its LDS slot (one lane per address, no-return LDS
+        // add: nothing waits on it; the sum is ((0 + t0) + t1) + .. in tile order)
+        __hip_atomic_fetch_add(lnp + feat_of(16 * kk + (c & 15), h), B[0], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
         opaque(c1);  // the running sums are due now: nothing of this chunk stays live for later
         opaque(c2);
       }
-      c1 += xor32(c1);
-      c2 += xor32(c2);
+      c1 = sum32(c1);
+      c2 = sum32(c2);
       c1 /= (float)H;
       c2 /= (float)H;
       // pass 2 unpacks h3 and recomputes xhat again: opaque copies keep the compiler from holding
@@ -501,19 +520,17 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
       EB_STAMP(5);
       gemm_cols(acc, op, lds + 3 * IMG_B, fresh_lane(lane));
-      relu_select(A, acc, a3);
+      cbarrier();
+      relu_select_pk(op, acc, a3);  // G2
       EB_STAMP(6);
     }
-    cbarrier();
-    op.set(A);  // G2
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
-    relu_select(A, acc, a2);
-    EB_STAMP(8);
     cbarrier();
-    op.set(A);  // G1
+    relu_select_pk(op, acc, a2);  // G1
+    EB_STAMP(8);
     pin(op);
     // de = G0 W_e + (g + g2) (mlp_bwd_res_kernel's add_grad_w order) needs the incoming rows
     // again: re-read now (L2) so the loads complete under the L1 hand-off and chain step.
@@ -534,10 +551,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     produce_pair(lds, nbase + 4 * gsz, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
     gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
-    relu_select(A, acc, a1);
-    EB_STAMP(10);
     cbarrier();
-    op.set(A);  // G0
+    relu_select_pk(op, acc, a1);  // G0
+    EB_STAMP(10);
     pin(op);
     op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));

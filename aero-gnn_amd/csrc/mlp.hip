@@ -287,13 +287,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
             uint4 mine[NR / 8];
             tile_load_chunks<4 * NT>(mine, reinterpret_cast<const bf16*>(a.seg[s].ptr) + (size_t)wave * 32 * a.seg[s].ld,
                                      a.rows - wave * 32, stg[threadIdx.x >> 6], lane, a.seg[s].ld / 8);
-#pragma unroll
-            for (int i = 0; i < NR / 8; ++i) {
-              float o[8];
-              unpack8_w(o, mine[i]);
-#pragma unroll
-              for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
-            }
+            b.set_w(mine);  // the operand from the chunks directly (no fp32 round trip)
             staged = true;
           }
         }
@@ -302,8 +296,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
           else load_segment<T, NR, IN_FULL>(v, a.seg[s], rr, valid, h);
         }
       }
+      bool staged_b = false;
+      if constexpr (STAGE && IN_FULL && MODE != M_NIN) staged_b = a.seg[s].kind == AGN_SEG_PLAIN;
       if (W2 && walk2 && s == 1) b = bagg;
-      else b.set(v);
+      else if (!staged_b) b.set(v);
       __syncthreads();
       if constexpr (IN_FULL) gemm<T, NT, NR, true>(acc, b, NUH, wl, NUH, NT, lane);
       else if constexpr (MODE == M_NIN) gemm<T, NT, NR, true>(acc, b, nu, wl, nu, NT, lane);
@@ -337,7 +333,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) s += (OUT_FULL || feat_of(i, h) < outd) ? acc[i / 16][i % 16] : 0.f;
-      s += xor32(s);
+      s = sum32(s);
       mean = s / (float)outd;
       float q = 0.f;
 #pragma unroll
@@ -345,7 +341,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
         const float d = acc[i / 16][i % 16] - mean;
         if (OUT_FULL || feat_of(i, h) < outd) q = ln_sq_acc(q, d);
       }
-      q += xor32(q);
+      q = sum32(q);
       rstd = 1.0f / sqrtf(q / (float)outd + 1e-5f);
       if (a.stats && valid && h == 0) {
         a.stats[2 * (size_t)row] = mean;
@@ -496,8 +492,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
         B[4 * q + e] = A[4 * q + e] * xh;  // g * xhat (LN weight-grad partial)
       }
     }
-    c1 += xor32(c1);
-    c2 += xor32(c2);
+    c1 = sum32(c1);
+    c2 = sum32(c2);
     c1 /= (float)M;
     c2 /= (float)M;
     if (a.ln_partial) {  // LayerNorm parameter partials over the wave's 32 rows (butterfly)
@@ -722,23 +718,15 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     }
     FWD_STAMP(1);
     {
-      float v[NR];
       if (staged_in) {  // coalesced 1-KB loads through the wave's LDS staging rows
         tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
                                lane);
         uint4 mine[NR / 8];
         tile_load_finish<H / 8>(mine, eraw, stg[threadIdx.x >> 6], lane);
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) {
-          float o[8];
-          unpack8_w(o, mine[i]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
-        }
+        b.set_w(mine);
       } else {
-        load_row_w<T, NR>(v, reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
+        b.load_w(reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
       }
-      b.set(v);
     }
     // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
     // operand instead of re-reading the row in the epilogue
@@ -767,7 +755,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
-      s += xor32(s);
+      s = sum32(s);
       mean = s / (float)H;
       float q = 0.f;
 #pragma unroll
@@ -775,7 +763,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         const float d = acc[i / 16][i % 16] - mean;
         q = ln_sq_acc(q, d);
       }
-      q += xor32(q);
+      q = sum32(q);
       rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
       if (a.stats && valid && h == 0) {
         a.stats[2 * (size_t)row] = mean;
@@ -941,8 +929,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
           }
         }
       }
-      c1 += xor32(c1);
-      c2 += xor32(c2);
+      c1 = sum32(c1);
+      c2 = sum32(c2);
       c1 /= (float)H;
       c2 /= (float)H;
       if (a.ln_partial) {

@@ -79,16 +79,8 @@ __global__ __launch_bounds__(PJ_BLOCK, 2) void proj_kernel(int rows, const bf16*
         uint4 mine[NR / 8];
         tile_load_chunks<H / 8>(mine, (s == 0 ? x0 : x1) + (size_t)tile * 32 * x_ld, rows - tile * 32, stg[wid], lane,
                                 x_ld / 8);
-        float v[NR];
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) {
-          float o[8];
-          unpack8_w(o, mine[i]);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[8 * i + e] = o[e];
-        }
         BOp<bf16, NR> b;
-        b.set(v);
+        b.set_w(mine);
         gemm<bf16, NT, NR, true>(acc, b, 8, w + ((size_t)grp * NT * KU + 8 * s) * 64, KU, NT, lane);
       }
       uint4 res[NR / 8];

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export AEROGNN_MEMLOG=0
 T=${1:-r4a}
 rc=0
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rP --timeout 300 --timeout-method thread \
     > gpurun_out/${T}_gpu_tests.log 2>&1 || rc=$?
 tail -3 gpurun_out/${T}_gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "gpu tests ended with status $rc"; exit $rc; fi
