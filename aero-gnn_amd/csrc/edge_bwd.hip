@@ -241,18 +241,20 @@ AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<b
 // activation (relu outputs are +0 or positive int16 patterns: 0 - a is negative exactly when a > 0,
 // and its arithmetic shift by 15 is 0xffff or 0). Bitwise the select-then-round of the split path:
 // a dropped element is 0x0000 either way, a kept one is the same rounding of dA.
-typedef short s16x2v __attribute__((ext_vector_type(2)));
+// The mask is built on the whole 8-lane short vector: the per-dword form
+// bit_cast<short2>(bit_cast<uint4>(act)[k]) is miscompiled by this hipcc (ROCm 7.2, -O3: dword 0's
+// mask is applied to all four dwords of the unit; caught by test_fused_edge_bwd_matches_split and
+// the bf16 oracle tests, reproduced in a 20-line kernel).
+typedef short s16x8v __attribute__((ext_vector_type(8)));
 AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const BOp<bf16, NR>& act) {
 #pragma unroll
   for (int i = 0; i < NR / 8; ++i) {
-    const u32x4 a = __builtin_bit_cast(u32x4, act.u[i]);
+    const u32x4 m = __builtin_bit_cast(u32x4, (s16x8v{} - __builtin_bit_cast(s16x8v, act.u[i])) >> 15);
     u32x4 w;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = 8 * i + 2 * k;
-      const uint32_t p = pack2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]);
-      const s16x2v neg = s16x2v{0, 0} - __builtin_bit_cast(s16x2v, a[k]);
-      w[k] = p & __builtin_bit_cast(uint32_t, neg >> s16x2v{15, 15});
+      w[k] = pack2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]) & m[k];
     }
     out.u[i] = __builtin_bit_cast(bf16x8, w);
   }

@@ -9,7 +9,7 @@
 #define REP64(x) REP8(REP8(x))
 
 template <int KIND>
-__global__ void k(float* out, unsigned long long* cyc, int iters) {
+__global__ void k(float* out, unsigned long long* cyc, int iters, unsigned long long smask) {
   float a0 = threadIdx.x, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
   float b = 1.0001f, c = 0.5f;
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -55,6 +55,20 @@ __global__ void k(float* out, unsigned long long* cyc, int iters) {
       REP8(asm volatile("v_permlane32_swap_b32 %0, %1\n v_permlane32_swap_b32 %2, %3\n v_permlane32_swap_b32 %4, %5\n v_permlane32_swap_b32 %6, %7\n"
                         "v_permlane32_swap_b32 %0, %1\n v_permlane32_swap_b32 %2, %3\n v_permlane32_swap_b32 %4, %5\n v_permlane32_swap_b32 %6, %7"
                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));)
+    } else if constexpr (KIND == 10) {  // v_cndmask_b32_e64 with an SGPR-pair mask (the compiler's form)
+      REP8(asm volatile("v_cndmask_b32_e64 %0, %0, %8, %9\n v_cndmask_b32_e64 %1, %1, %8, %9\n v_cndmask_b32_e64 %2, %2, %8, %9\n v_cndmask_b32_e64 %3, %3, %8, %9\n"
+                        "v_cndmask_b32_e64 %4, %4, %8, %9\n v_cndmask_b32_e64 %5, %5, %8, %9\n v_cndmask_b32_e64 %6, %6, %8, %9\n v_cndmask_b32_e64 %7, %7, %8, %9"
+                        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b), "s"(smask));)
+    } else if constexpr (KIND == 11) {  // v_mov_b32_dpp quad_perm identity with a bank mask (lane merge)
+      REP8(asm volatile("v_mov_b32_dpp %0, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n v_mov_b32_dpp %1, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n"
+                        "v_mov_b32_dpp %2, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n v_mov_b32_dpp %3, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n"
+                        "v_mov_b32_dpp %4, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n v_mov_b32_dpp %5, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n"
+                        "v_mov_b32_dpp %6, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n v_mov_b32_dpp %7, %8 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc"
+                        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));)
+    } else if constexpr (KIND == 12) {  // v_mov_b32 (register copies)
+      REP8(asm volatile("v_mov_b32 %0, %8\n v_mov_b32 %1, %8\n v_mov_b32 %2, %8\n v_mov_b32 %3, %8\n"
+                        "v_mov_b32 %4, %8\n v_mov_b32 %5, %8\n v_mov_b32 %6, %8\n v_mov_b32 %7, %8"
+                        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "v"(b));)
     } else if constexpr (KIND == 9) {  // v_pk_max_i16 / v_and (integer)
       REP8(asm volatile("v_pk_max_i16 %0, %0, 0\n v_pk_max_i16 %1, %1, 0\n v_pk_max_i16 %2, %2, 0\n v_pk_max_i16 %3, %3, 0\n"
                         "v_and_b32 %4, %4, %8\n v_and_b32 %5, %5, %8\n v_and_b32 %6, %6, %8\n v_and_b32 %7, %7, %8"
@@ -73,8 +87,8 @@ void run(const char* name, int threads) {
   unsigned long long* cyc;
   hipMalloc(&out, blocks * threads * sizeof(float));
   hipMalloc(&cyc, blocks * (threads / 64) * sizeof(unsigned long long));
-  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(threads), 0, 0, out, cyc, 10);
-  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(threads), 0, 0, out, cyc, iters);
+  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(threads), 0, 0, out, cyc, 10, 0x5555555555555555ull);
+  hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(threads), 0, 0, out, cyc, iters, 0x5555555555555555ull);
   hipDeviceSynchronize();
   const int n = blocks * (threads / 64);
   unsigned long long* h = new unsigned long long[n];
@@ -100,6 +114,9 @@ int main() {
     run<5>("v_add_f32_dpp", t);
     run<6>("v_cndmask_b32", t);
     run<9>("v_pk_max_i16/v_and", t);
+    run<10>("v_cndmask_b32_e64 sgpr", t);
+    run<11>("v_mov_b32_dpp bankmask", t);
+    run<12>("v_mov_b32", t);
   }
   return 0;
 }
