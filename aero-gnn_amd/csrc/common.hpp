@@ -682,6 +682,28 @@ AGN_DEV float ln_bwd_out(float g, float gm, float c1, float c2, float xh, float 
   const float t = __builtin_fmaf(g, gm, -c1);
   return __builtin_fmaf(-xh, c2, t) * rstd;
 }
+// The same steps on two consecutive registers with the elementwise work in packed fp32
+// (v_pk_mul / v_pk_add / v_pk_fma: one instruction per pair, the scalar rounding per element;
+// a lone wave issues them at the scalar rate, so they halve its VALU time). The running sums c1,
+// c2 still take the elements in register order. Contraction off: no fma the scalar forms lack.
+AGN_DEV f32x2 ln_xhat2(f32x2 hv, float mean, float rstd) {
+#pragma clang fp contract(off)
+  return (hv - f32x2{mean, mean}) * f32x2{rstd, rstd};
+}
+AGN_DEV void ln_bwd_acc2(float& c1, float& c2, f32x2 g, f32x2 gm, f32x2 xh) {
+#pragma clang fp contract(off)
+  const f32x2 gg = g * gm;
+  c1 = c1 + gg[0];
+  c2 = __builtin_fmaf(gg[0], xh[0], c2);
+  c1 = c1 + gg[1];
+  c2 = __builtin_fmaf(gg[1], xh[1], c2);
+}
+AGN_DEV f32x2 ln_bwd_out2(f32x2 g, f32x2 gm, float c1, float c2, f32x2 xh, float rstd) {
+#pragma clang fp contract(off)
+  const f32x2 t = __builtin_elementwise_fma(g, gm, f32x2{-c1, -c1});
+  return __builtin_elementwise_fma(-xh, f32x2{c2, c2}, t) * f32x2{rstd, rstd};
+}
+AGN_DEV f32x2 f2(float x, float y) { return f32x2{x, y}; }
 
 // ---------------------------------------------------------------- wave reductions
 // The value a butterfly partner at distance M holds, with VALU cross-lane operations (no LDS

@@ -419,7 +419,11 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       unpack8_w(o, graw[i]);  // load8_w's exchange + conversion
       unpack8_w(o2, g2raw[i]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) A[8 * i + e] = o[e] + o2[e];
+      for (int e = 0; e < 8; e += 2) {
+        const f32x2 sv = f2(o[e], o[e + 1]) + f2(o2[e], o2[e + 1]);  // v_pk_add
+        A[8 * i + e] = sv[0];
+        A[8 * i + e + 1] = sv[1];
+      }
     }
     if (!valid) {
 #pragma unroll
@@ -445,11 +449,14 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
           for (int j = 0; j < 2; ++j) {
             const f32x4 gm = *reinterpret_cast<const f32x4*>(gmv + 16 * i + 8 * j + 4 * h);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
+            for (int e = 0; e < 4; e += 2) {
               const int r = 8 * i + 4 * j + e;
-              const float xh = (hv[4 * j + e] - mean) * rstd;
-              ln_bwd_acc(c1, c2, A[r], gm[e], xh);
-              B[r - 16 * kk] = A[r] * xh;
+              const f32x2 xh = ln_xhat2(f2(hv[4 * j + e], hv[4 * j + e + 1]), mean, rstd);
+              const f32x2 g = f2(A[r], A[r + 1]);
+              ln_bwd_acc2(c1, c2, g, f2(gm[e], gm[e + 1]), xh);
+              const f32x2 bx = g * xh;
+              B[r - 16 * kk] = bx[0];
+              B[r + 1 - 16 * kk] = bx[1];
             }
           }
         }
@@ -487,10 +494,12 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int j = 0; j < 2; ++j) {
           const f32x4 gm = *reinterpret_cast<const f32x4*>(gmv2 + 16 * i + 8 * j + 4 * h);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int e = 0; e < 4; e += 2) {
             const int r = 8 * i + 4 * j + e;
-            const float xh = (hv[4 * j + e] - mean) * rstd;
-            A[r] = ln_bwd_out(A[r], gm[e], c1, c2, xh, rstd);
+            const f32x2 xh = ln_xhat2(f2(hv[4 * j + e], hv[4 * j + e + 1]), mean, rstd);
+            const f32x2 o = ln_bwd_out2(f2(A[r], A[r + 1]), f2(gm[e], gm[e + 1]), c1, c2, xh, rstd);
+            A[r] = o[0];
+            A[r + 1] = o[1];
           }
         }
       }
@@ -567,9 +576,11 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         unpack8_w(x, graw[i]);
         unpack8_w(y, g2raw[i]);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float t = acc[(8 * i + e) / 16][(8 * i + e) % 16];
-          v[8 * i + e] = a.g ? t + (x[e] + y[e]) : t + y[e];
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 t = f2(acc[(8 * i + e) / 16][(8 * i + e) % 16], acc[(8 * i + e + 1) / 16][(8 * i + e + 1) % 16]);
+          const f32x2 o = a.g ? t + (f2(x[e], x[e + 1]) + f2(y[e], y[e + 1])) : t + f2(y[e], y[e + 1]);
+          v[8 * i + e] = o[0];
+          v[8 * i + e + 1] = o[1];
         }
       }
       store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);

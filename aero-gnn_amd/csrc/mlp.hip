@@ -954,9 +954,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
           for (int e = 0; e < 4; ++e) {
             const int r = 8 * i + 4 * j + e;
             const float xh = (hv[4 * j + e] - mean) * rstd;
-            // (= ln_bwd_out: hipcc emits fma(A, gm, -c1), fma(-xh, c2, .), * rstd here; the explicit
-            // helper makes this kernel spill 19 registers, so the expression stays)
-            A[r] = (A[r] * gm[e] - c1 - xh * c2) * rstd;
+            A[r] = ln_bwd_out(A[r], gm[e], c1, c2, xh, rstd);
           }
         }
       }
