@@ -704,6 +704,23 @@ AGN_DEV f32x2 ln_bwd_out2(f32x2 g, f32x2 gm, float c1, float c2, f32x2 xh, float
   return __builtin_elementwise_fma(-xh, f32x2{c2, c2}, t) * f32x2{rstd, rstd};
 }
 AGN_DEV f32x2 f2(float x, float y) { return f32x2{x, y}; }
+// variance pass of the statistics on a register pair: q += d0^2, q += d1^2 (ln_sq_acc in register
+// order), the two subtractions of the mean in one v_pk_add
+AGN_DEV float ln_sq_acc2(float q, float v0, float v1, float mean) {
+#pragma clang fp contract(off)
+  const f32x2 d = f32x2{v0, v1} - f32x2{mean, mean};
+  q = __builtin_fmaf(d[0], d[0], q);
+  return __builtin_fmaf(d[1], d[1], q);
+}
+// LayerNorm output gamma * xhat + beta as an explicit fma of the rounded xhat (every kernel)
+AGN_DEV float ln_out(float v, float mean, float rstd, float g, float b) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf((v - mean) * rstd, g, b);
+}
+AGN_DEV f32x2 ln_out2(f32x2 v, float mean, float rstd, f32x2 g, f32x2 b) {
+#pragma clang fp contract(off)
+  return __builtin_elementwise_fma((v - f32x2{mean, mean}) * f32x2{rstd, rstd}, g, b);
+}
 
 // ---------------------------------------------------------------- wave reductions
 // The value a butterfly partner at distance M holds, with VALU cross-lane operations (no LDS

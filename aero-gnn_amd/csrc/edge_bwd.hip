@@ -394,10 +394,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       mean = s / (float)H;
       float q = 0.f;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        const float d = acc[i / 16][i % 16] - mean;
-        q = ln_sq_acc(q, d);
-      }
+      for (int i = 0; i < NR; i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
       q = sum32(q);
       rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
     }

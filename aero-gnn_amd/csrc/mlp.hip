@@ -369,7 +369,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
             const f32x4 g4 = *reinterpret_cast<const f32x4*>(a.ln_g + f0);
             const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.ln_b + f0);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v8[4 * j + e] = (v8[4 * j + e] - mean) * rstd * g4[e] + b4[e];
+            for (int e = 0; e < 4; ++e) v8[4 * j + e] = ln_out(v8[4 * j + e], mean, rstd, g4[e], b4[e]);
           }
         }
         if (rp) {
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
           for (int e = 0; e < 4; ++e)
             if (f0 + e < outd) { g4[e] = a.ln_g[f0 + e]; b4[e] = a.ln_b[f0 + e]; }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (v[e] - mean) * rstd * g4[e] + b4[e];
+          for (int e = 0; e < 4; ++e) v[e] = ln_out(v[e], mean, rstd, g4[e], b4[e]);
         }
         if (rp) {
           const f32x4 r = load4_masked(rp, f0, outd, false);
@@ -759,10 +759,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       mean = s / (float)H;
       float q = 0.f;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        const float d = acc[i / 16][i % 16] - mean;
-        q = ln_sq_acc(q, d);
-      }
+      for (int i = 0; i < NR; i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
       q = sum32(q);
       rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
       if (a.stats && valid && h == 0) {
@@ -790,7 +787,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
           const f32x4 g4 = *reinterpret_cast<const f32x4*>(&pv[RES_MAXL][f0]);
           const f32x4 b4 = *reinterpret_cast<const f32x4*>(&pv[RES_MAXL + 1][f0]);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[4 * j + e] = (v[4 * j + e] - mean) * rstd * g4[e] + b4[e];
+          for (int e = 0; e < 4; e += 2) {  // packed fp32: ln_out per element
+            const f32x2 o = ln_out2(f2(v[4 * j + e], v[4 * j + e + 1]), mean, rstd, f2(g4[e], g4[e + 1]),
+                                    f2(b4[e], b4[e + 1]));
+            v[4 * j + e] = o[0];
+            v[4 * j + e + 1] = o[1];
+          }
         }
       }
       if (rp) {
@@ -798,7 +800,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         if (res_in) e0.get8(r, i);
         else load8_w(r, rp, i, h);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = round_t<T>(v[e]) + r[e];
+        for (int e = 0; e < 8; e += 2) {  // round_t(v) + r, the add packed
+          const uint32_t p = pack2t<T>(v[e], v[e + 1]);
+          const f32x2 o = f2(lo16<T>(p), hi16<T>(p)) + f2(r[e], r[e + 1]);
+          v[e] = o[0];
+          v[e + 1] = o[1];
+        }
       }
       store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
     }
