@@ -665,6 +665,39 @@ AGN_DEV void gemm(f32x16 (&acc)[NT], const BOp<T, NR>& b, int nu, const uint4* l
   }
 }
 
+// ---------------------------------------------------------------- exact row sums on the MFMA
+// x + y of two bf16 rows, into acc-layout fp32 registers, by the matrix cores: an identity A
+// fragment times the row operand (acc order, BOp::set_w) is the row itself, exactly (one nonzero
+// product per output); four MFMAs per 32-feature tile give acc = x exactly, then round(x + y) -
+// the fp32 add of the VALU path, bit for bit (a -0 sum comes out +0, equal as a value; a NaN or
+// inf in one feature reaches the 15 other features of its k-step through 0 * inf).
+// A operand lane map (cdna_hip_programming.md: lane l holds A[row l&31][k = 8(l>>5) + j]); the
+// operand's k order is the acc-register order (feature 16u + 8(j>>2) + 4(l>>5) + (j&3) at k-step
+// u), so the identity's one for output row i < 16 of k-step 2 ot sits at j = 4(i>>3) + (i&3) of the
+// lanes with (i>>2)&1 == l>>5; rows 16..31 take the same pattern in k-step 2 ot + 1.
+AGN_DEV void ident_frags(bf16x8& f0, bf16x8& f1, int lane) {
+  const int i = lane & 31, il = i & 15;
+  const int j = 4 * (il >> 3) + (il & 3);
+  const uint32_t one = (((il >> 2) & 1) == (lane >> 5)) ? (0x3F80u << (16 * (j & 1))) : 0u;
+  const int d = j >> 1;
+  const u32x4 w = {d == 0 ? one : 0u, d == 1 ? one : 0u, d == 2 ? one : 0u, d == 3 ? one : 0u};
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  f0 = __builtin_bit_cast(bf16x8, i < 16 ? w : z);
+  f1 = __builtin_bit_cast(bf16x8, i < 16 ? z : w);
+}
+template <int NT, int NR>
+AGN_DEV void acc_add2_mfma(f32x16 (&acc)[NT], const BOp<bf16, NR>& x, const BOp<bf16, NR>& y, const bf16x8& f0,
+                           const bf16x8& f1) {
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, x.u[2 * ot], f32x16{}, 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, x.u[2 * ot + 1], acc[ot], 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, y.u[2 * ot], acc[ot], 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, y.u[2 * ot + 1], acc[ot], 0, 0, 0);
+}
+
 // ---------------------------------------------------------------- LayerNorm element steps
 // Written with explicit fused operations: under -ffp-contract=fast the compiler's SLP
 // vectorisation otherwise contracts some elements of a row (fma) and not others (packed mul +

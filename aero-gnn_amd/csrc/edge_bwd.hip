@@ -344,15 +344,13 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     f32x16 acc[NT];
     BOp<bf16, NR> a1;  // the only activation kept from the forward pass
     {
-      const bf16* ps = P + (size_t)sid * (2 * H);
-      const bf16* pd = P + (size_t)did * (2 * H) + H;
-#pragma unroll
-      for (int i = 0; i < NR / 8; ++i) {
-        float x[8], y[8];
-        load8_w(x, ps, i, h);
-        load8_w(y, pd, i, h);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
+      {  // acc = P_s[src] + P_d[dst] on the matrix cores (the forward kernel's exact add)
+        BOp<bf16, NR> xs, xd;
+        xs.load_w(P + (size_t)sid * (2 * H), h);
+        xd.load_w(P + (size_t)did * (2 * H) + H, h);
+        bf16x8 f0, f1;
+        ident_frags(f0, f1, fresh_lane(lane));
+        acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
       }
       BOp<bf16, NR> eop;
       eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
@@ -410,17 +408,15 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     // ---- incoming gradient S = g + dAgg[dst] (mlp_bwd_res_kernel's load_grad_w)
     float A[NR];
+    {  // S = g + g2 on the matrix cores (exact fp32 add): acc is free once h3 is packed
+      BOp<bf16, NR> og, og2;
+      og.set_w(graw);
+      og2.set_w(g2raw);
+      bf16x8 f0, f1;
+      ident_frags(f0, f1, fresh_lane(lane));
+      acc_add2_mfma<NT, NR>(acc, og, og2, f0, f1);
 #pragma unroll
-    for (int i = 0; i < NR / 8; ++i) {
-      float o[8], o2[8];
-      unpack8_w(o, graw[i]);  // load8_w's exchange + conversion
-      unpack8_w(o2, g2raw[i]);
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        const f32x2 sv = f2(o[e], o[e + 1]) + f2(o2[e], o2[e + 1]);  // v_pk_add
-        A[8 * i + e] = sv[0];
-        A[8 * i + e + 1] = sv[1];
-      }
+      for (int i = 0; i < NR; ++i) A[i] = acc[i / 16][i % 16];
     }
     if (!valid) {
 #pragma unroll

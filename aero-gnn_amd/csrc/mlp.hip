@@ -703,16 +703,13 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         ndst = a.dst[rn];
       }
       const T* P = reinterpret_cast<const T*>(a.proj);
-      const T* ps = P + (size_t)cs * (2 * H);
-      const T* pd = P + (size_t)cd * (2 * H) + H;
-#pragma unroll
-      for (int i = 0; i < NR / 8; ++i) {
-        float x[8], y[8];
-        load8_w(x, ps, i, h);
-        load8_w(y, pd, i, h);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[(8 * i + e) / 16][(8 * i + e) % 16] = x[e] + y[e];
-      }
+      // acc = P_s[src] + P_d[dst] on the matrix cores (exact fp32 add, common.hpp acc_add2_mfma)
+      BOp<T, NR> xs, xd;
+      xs.load_w(P + (size_t)cs * (2 * H), h);
+      xd.load_w(P + (size_t)cd * (2 * H) + H, h);
+      bf16x8 f0, f1;
+      ident_frags(f0, f1, lane);
+      acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
     } else {
       acc_bias_lds<NT>(acc, pv[0], h);
     }
