@@ -55,7 +55,8 @@ constexpr int OFF_RING = 4 * IMG_B;
 constexpr int OFF_PV = OFF_RING + NSLOT * SLOT_B;  // fp32 [4][H]: b1, b2, b3, LN gamma
 constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[4], consumed[4]
 constexpr int OFF_LNP = OFF_FLAG + 32;             // fp32 [CW][2][H]: LayerNorm partials per chain wave
-constexpr int LDS_B = OFF_LNP + CW * 2 * H * 4;
+constexpr int OFF_IDS = OFF_LNP + CW * 2 * H * 4;   // int [CW][64]: next tile's src (lanes 0-31) / dst
+constexpr int LDS_B = OFF_IDS + CW * 64 * 4;
 static_assert(LDS_B <= 160 * 1024, "LDS budget");
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -203,6 +204,9 @@ struct Rounds {  // XCD-grouped round walk (blocks b and b + 8 share an XCD and 
 // over at once (items n0, n0 + 1): every lane writes, each half into its own slot.
 AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<bf16, NR>& X, int lane,
                           unsigned long long* ist = nullptr) {
+#ifdef AGN_EB_NORING
+  return;  // diagnostic build only: the chain alone (no hand-offs; dW / db are not computed)
+#endif
   int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
   int* consumed = filled + 4;
   const int k0 = n0 % NSLOT, j0 = n0 / NSLOT;
@@ -292,16 +296,21 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   const float* pv = reinterpret_cast<const float*>(lds + OFF_PV);
   const bf16* P = reinterpret_cast<const bf16*>(a.proj);
   int rcount = 0;
-  // the node ids of a wave's next tile are loaded one tile ahead: the tile's P_s / P_d gathers
-  // then wait for one memory latency instead of two dependent ones
-  auto tile_ids = [&](int rd, int& sid, int& did) {
+  // The node ids of a wave's next tile are loaded one tile ahead (the tile's P_s / P_d gathers
+  // then wait for one memory latency instead of two dependent ones) and handed to the next tile
+  // through the wave's LDS slot, not a loop-carried register: a loop-carried load result makes
+  // the compiler's wait at the loop head vmcnt(0), i.e. for this tile's de / G0 stores as well.
+  // Lane l loads the src (l < 32) or dst (l >= 32) of row l & 31.
+  int* ids = reinterpret_cast<int*>(lds + OFF_IDS) + cw * 64;
+  const int32_t* const srcp = a.src;  // (scalar copies: a per-lane choice of the struct field made
+  const int32_t* const dstp = a.dst;  // the compiler load the pointer itself, behind a full wait)
+  auto tile_id = [&](int rd) {
     const int row = (rd * CW + cw) * 32 + (lane0 & 31);
     const int rr = row < a.rows ? row : a.rows - 1;
-    sid = a.src[rr];
-    did = a.dst[rr];
+    const int32_t* p = lane0 < 32 ? srcp : dstp;
+    return p[rr];
   };
-  int sid_next = 0, did_next = 0;
-  if (rw.first < rw.end) tile_ids(rw.first, sid_next, did_next);
+  if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
 
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
@@ -323,7 +332,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
-    const int sid = sid_next, did = did_next;
+    const int sid = ids[c], did = ids[32 + c];
+    const bool more = rd + rw.step < rw.end;
+    const int nid = tile_id(more ? rd + rw.step : rd);  // stored to the slot before the tile's stores
     // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
     // forward recompute
     uint4 graw[NR / 8], g2raw[NR / 8];
@@ -559,6 +570,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     relu_select_pk(op, acc, a1);  // G0
     EB_STAMP(10);
     pin(op);
+    if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
     op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     {
@@ -578,7 +590,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       }
       store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
     }
-    if (rd + rw.step < rw.end) tile_ids(rd + rw.step, sid_next, did_next);
     EB_STAMP(11);
 #ifdef AGN_EB_STAMPS
     ++ntile_done;
@@ -588,6 +599,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
 
 // ------------------------------------------------------------------------------ dW wave
 AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
+#ifdef AGN_EB_NORING
+  return;  // diagnostic build only (see produce_pair)
+#endif
   int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
   int* consumed = filled + 4;
   const int ntiles = (a.rows + 31) / 32;

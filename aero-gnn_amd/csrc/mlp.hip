@@ -661,6 +661,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
   __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e loads
+  __shared__ int ids[RES_WPB][64];                     // per-wave next-tile src (lanes 0-31) / dst
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
@@ -668,14 +669,20 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   const int ntiles = (a.rows + 31) / 32;
   const agn_seg& sg = a.seg[0];
   const ResTiles tw(ntiles, threadIdx.x >> 6);
-  // the sender / receiver ids of the wave's next tile are loaded one tile ahead, so a tile's
-  // projection-row gathers issue together with its e loads (one memory latency per tile, not two)
-  int nsrc = 0, ndst = 0;
-  if (a.proj && tw.first < tw.end) {
-    const int r0 = min(tw.first * 32 + (lane0 & 31), a.rows - 1);
-    nsrc = a.src[r0];
-    ndst = a.dst[r0];
-  }
+  // The sender / receiver ids of the wave's next tile are loaded one tile ahead, so a tile's
+  // projection-row gathers issue together with its e loads (one memory latency per tile, not two).
+  // They reach the next tile through the wave's LDS slot, not a loop-carried register: a
+  // loop-carried load result makes the compiler wait vmcnt(0) at the loop head, i.e. also for the
+  // previous tile's e' stores. Lane l loads the src (l < 32) or dst (l >= 32) of row l & 31.
+  int* wids = ids[threadIdx.x >> 6];
+  const int32_t* const srcp = a.src;
+  const int32_t* const dstp = a.dst;
+  // (without projections the load reads the input rows instead: always a valid address, so the
+  // next-id load below needs no branch - a conditional load leaves a register write at the loop
+  // head that the compiler guards with vmcnt(0))
+  const int32_t* const idp = a.proj ? (lane0 < 32 ? srcp : dstp) : reinterpret_cast<const int32_t*>(sg.ptr);
+  auto tile_id = [&](int t) { return idp[min(t * 32 + (lane0 & 31), a.rows - 1)]; };
+  if (a.proj && tw.first < tw.end) wids[lane0] = tile_id(tw.first);
 #ifdef AGN_FWD_STAMPS
   int ntile = 0;
 #endif
@@ -695,13 +702,10 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     // rows (issuing the e loads ahead of the gathers measured slower: DESIGN.md §9, round 3)
     const bool staged_in = sg.ld == H;
     uint4 eraw[NR / 8];
+    const bool more = a.proj && tile + tw.step < tw.end;
+    const int nid = tile_id(more ? tile + tw.step : tile);  // (unconditional: see tile_id)
     if (a.proj) {
-      const int cs = nsrc, cd = ndst;
-      if (tile + tw.step < tw.end) {
-        const int rn = min((tile + tw.step) * 32 + c, a.rows - 1);
-        nsrc = a.src[rn];
-        ndst = a.dst[rn];
-      }
+      const int cs = wids[c], cd = wids[32 + c];
       const T* P = reinterpret_cast<const T*>(a.proj);
       // acc = P_s[src] + P_d[dst] on the matrix cores (exact fp32 add, common.hpp acc_add2_mfma)
       BOp<T, NR> xs, xd;
@@ -804,6 +808,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
           v[e + 1] = o[1];
         }
       }
+      if (i == 0 && more) wids[lane] = nid;  // (the slot's reads are done: LDS is in order per wave)
       store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
     }
     FWD_STAMP(11);
