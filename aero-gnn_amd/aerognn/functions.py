@@ -498,7 +498,16 @@ class GMPFn(torch.autograd.Function):
         if spec.trick:
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
             dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
-            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
+            dPd = torch.empty(N, H, dtype=dt, device=dev)
+            if fused:
+                # dW_e = G0^T e, with the receiver sums dP_d of G0 (edges are receiver-sorted, so the
+                # groups are contiguous row ranges) from the same pass over G0
+                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
+                we = WGrad()
+                we.add(g0, e, dwe, seg=(lv.rowptr, dPd))
+                we.run()
+            else:
+                segment_sum(N, H, lv.rowptr, None, g0, dPd)
             if proj_kernel_ok(dx, H):
                 s_el = dx.element_size()
                 proj_backward(N, dPs, dPd, spec.pack["projT"], dx, tag="proj_bwd",
@@ -513,10 +522,6 @@ class GMPFn(torch.autograd.Function):
             # different row counts leaves most workgroups idle behind the edge descs (measured)
             wg = WGrad()
             if fused:
-                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
-                we = WGrad()
-                we.add(g0, e, dwe)
-                we.run()
                 eg = [dwe]
                 for l in range(3):
                     eg += [dW13[l], db13[l]]

@@ -156,9 +156,68 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
   return r;
 }
 
+// Segment sums of the stage's G rows (agn_wgrad_desc.seg_*): the groups whose first row lies in
+// this stage and in this block's row range (plus, in the block that ends the rows, the trailing
+// empty groups) are summed by 16-thread teams, 8 features per thread, each group's rows in order
+// from its first row - from the staged LDS tile while they are in it, from G in memory past it
+// (the group that runs into the next stage or block) - so every sum is agn_segment_sum's.
+template <typename T>
+AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, int r0, int sr_end, int& gcur, int g_hi, int stage_end,
+                       bool last) {
+  constexpr int LD = DwTile<T>::LD;
+  const int team = threadIdx.x >> 4, f0 = 8 * (threadIdx.x & 15);
+  const T* G = reinterpret_cast<const T*>(d.g);
+  T* out = reinterpret_cast<T*>(d.seg_out);
+  while (gcur < g_hi) {
+    // groups starting before stage_end (all of them in the block's last stage), up to 256 at once
+    const int gi = gcur + (int)threadIdx.x;
+    const bool in = gi < g_hi && (last || d.seg_ptr[gi] < stage_end);
+    const int cnt = __syncthreads_count(in);
+    if (cnt == 0) break;
+    for (int g = gcur + team; g < gcur + cnt; g += DW_THREADS / 16) {
+      const int beg = d.seg_ptr[g], end = d.seg_ptr[g + 1];
+      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int j = beg; j < end; ++j) {
+        const T* p = (j < sr_end) ? sg + (j - r0) * LD + f0 : G + (size_t)j * d.ldg + f0;
+        const uint4 raw = *reinterpret_cast<const uint4*>(p);
+        float x[8];
+        if constexpr (sizeof(T) == 2) {
+          const u32x4 w = __builtin_bit_cast(u32x4, raw);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            x[2 * q] = lo16<T>(w[q]);
+            x[2 * q + 1] = hi16<T>(w[q]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] = 0.f;  // (seg sums are 16-bit only: agn_wgrad rejects fp32)
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += x[q];
+      }
+      *reinterpret_cast<uint4*>(out + (size_t)g * d.seg_ld + f0) =
+          __builtin_bit_cast(uint4, u32x4{pack2t<T>(s[0], s[1]), pack2t<T>(s[2], s[3]), pack2t<T>(s[4], s[5]),
+                                          pack2t<T>(s[6], s[7])});
+    }
+    gcur += cnt;
+    if (cnt < DW_THREADS) break;
+  }
+}
+
+// first index g in [lo, hi) with ptr[g] >= v (hi if none); ptr non-decreasing
+AGN_DEV int lower_bound_i32(const int32_t* ptr, int lo, int hi, int v) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (ptr[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // grid: x = row chunk (split), y = M block * nKb + K block, z = desc
-// XG: some desc has a gathered X (xidx); a separate instantiation keeps the plain path free of it
-template <typename T, bool XG>
+// XG: some desc has a gathered X (xidx); SEG: some desc has segment sums (seg_ptr). Separate
+// instantiations keep the plain path free of either.
+template <typename T, bool XG, bool SEG = false>
 __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
@@ -187,6 +246,15 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   float bsum = 0.f;
   __shared__ float bhalf[DW_BLK];
   StageRegs<T> rg, rx;
+  // segment sums: this block owns the groups starting in [rbeg, rend) (and, ending the rows, the
+  // trailing empty ones); only the first output block of a split walks them
+  const bool seg = SEG && d.seg_ptr && blockIdx.y == 0;
+  int gcur = 0, g_hi = 0;
+  if (seg) {
+    gcur = lower_bound_i32(d.seg_ptr, 0, d.seg_n, rbeg);
+    g_hi = rend >= d.rows ? d.seg_n : lower_bound_i32(d.seg_ptr, gcur, d.seg_n, rend);
+    if (rbeg >= rend) seg_stage<T>(d, sg, rbeg, rbeg, gcur, g_hi, rend, true);  // an empty split's groups
+  }
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
     rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled, XG ? d.xidx : nullptr);
@@ -199,6 +267,12 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
       rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, XG ? d.xidx : nullptr);
+    }
+    if constexpr (SEG) {
+      if (seg) {
+        const int stage_end = min(r0 + DW_ROWS, rend);
+        seg_stage<T>(d, sg, r0, stage_end, gcur, g_hi, stage_end, stage_end >= rend);
+      }
     }
     if (d.db_partial && kb == 0) {
       const int col = threadIdx.x & (DW_BLK - 1), q = threadIdx.x >> 7;
@@ -429,17 +503,29 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   }
   (void)total;
   dim3 grid(ns, maxblk, bb.n);
-  bool xg = false;
-  for (int i = 0; i < bb.n; ++i) xg = xg || bb.d[i].xidx != nullptr;
-#define AGN_WG(T)                                                                             \
-  do {                                                                                        \
-    if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns); \
-    else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);   \
+  bool xg = false, sg = false;
+  for (int i = 0; i < bb.n; ++i) {
+    xg = xg || bb.d[i].xidx != nullptr;
+    if (bb.d[i].seg_ptr) {
+      if (bb.d[i].g_tiled || bb.d[i].m != DW_BLK || !bb.d[i].seg_out || bb.d[i].seg_n < 0 || bb.d[i].seg_ld < DW_BLK ||
+          bb.d[i].seg_ld % 8 || dtype == AGN_F32)
+        return AGN_E_ARG;
+      sg = true;
+    }
+  }
+  if (xg && sg) return AGN_E_ARG;  // one special instantiation per launch
+#define AGN_WG(T)                                                                                     \
+  do {                                                                                                \
+    if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns);         \
+    else if (sg) hipLaunchKernelGGL((wgrad_kernel<T, false, true>), grid, dim3(DW_THREADS), 0, st, bb, ns); \
+    else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);           \
   } while (0)
   if (dtype == AGN_BF16) AGN_WG(bf16);
   else if (dtype == AGN_F16) AGN_WG(f16);
-  else if (dtype == AGN_F32) AGN_WG(float);
-  else return AGN_E_DTYPE;
+  else if (dtype == AGN_F32) {  // (no segment sums in fp32: rejected above)
+    if (xg) hipLaunchKernelGGL((wgrad_kernel<float, true>), grid, dim3(DW_THREADS), 0, st, bb, ns);
+    else hipLaunchKernelGGL((wgrad_kernel<float, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);
+  } else return AGN_E_DTYPE;
 #undef AGN_WG
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
   return launch_status();
