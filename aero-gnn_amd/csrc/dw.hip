@@ -156,49 +156,82 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
   return r;
 }
 
-// Segment sums of the stage's G rows (agn_wgrad_desc.seg_*): the groups whose first row lies in
-// this stage and in this block's row range (plus, in the block that ends the rows, the trailing
-// empty groups) are summed by 16-thread teams, 8 features per thread, each group's rows in order
-// from its first row - from the staged LDS tile while they are in it, from G in memory past it
-// (the group that runs into the next stage or block) - so every sum is agn_segment_sum's.
+// rows j0 .. j1-1 (8 features from f0) added in order into s
+template <typename T, int U>
+AGN_DEV void add_rows8(float (&s)[8], const T* base, size_t ld, int j0, int j1, int f0) {
+#pragma unroll U
+  for (int j = j0; j < j1; ++j) {
+    const u32x4 w = __builtin_bit_cast(u32x4, *reinterpret_cast<const uint4*>(base + (size_t)j * ld + f0));
+    float x[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      x[2 * q] = lo16<T>(w[q]);
+      x[2 * q + 1] = hi16<T>(w[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += x[q];
+  }
+}
+
+// Segment sums of G's rows (agn_wgrad_desc.seg_*), 16-bit G only, from the staged rows
+// [r0, se) of this block's range [., rend): a block owns the groups that start in its range (the
+// last block also the trailing empty ones). Each group is summed in row order from zero, as
+// agn_segment_sum does, by a 16-thread team (8 features a thread) over the stage's LDS rows; a
+// group running past the stage leaves its partial sum in LDS (scar, group id in *gcar) for team 0
+// to continue in the next stage, and one running past the block's range finishes from G in
+// memory (once per block). Every value is agn_segment_sum's bit for bit.
+#ifndef AGN_SEG_U
+#define AGN_SEG_U 4
+#endif
+constexpr int SEG_U = AGN_SEG_U;  // LDS row loads in flight per walk step
+
 template <typename T>
-AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, int r0, int sr_end, int& gcur, int g_hi, int stage_end,
-                       bool last) {
+AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, float* scar, int* gcar, int r0, int se, int rend,
+                       int& gcur, int g_hi) {
   constexpr int LD = DwTile<T>::LD;
   const int team = threadIdx.x >> 4, f0 = 8 * (threadIdx.x & 15);
   const T* G = reinterpret_cast<const T*>(d.g);
   T* out = reinterpret_cast<T*>(d.seg_out);
-  while (gcur < g_hi) {
-    // groups starting before stage_end (all of them in the block's last stage), up to 256 at once
-    const int gi = gcur + (int)threadIdx.x;
-    const bool in = gi < g_hi && (last || d.seg_ptr[gi] < stage_end);
-    const int cnt = __syncthreads_count(in);
-    if (cnt == 0) break;
-    for (int g = gcur + team; g < gcur + cnt; g += DW_THREADS / 16) {
-      const int beg = d.seg_ptr[g], end = d.seg_ptr[g + 1];
-      float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int j = beg; j < end; ++j) {
-        const T* p = (j < sr_end) ? sg + (j - r0) * LD + f0 : G + (size_t)j * d.ldg + f0;
-        const uint4 raw = *reinterpret_cast<const uint4*>(p);
-        float x[8];
-        if constexpr (sizeof(T) == 2) {
-          const u32x4 w = __builtin_bit_cast(u32x4, raw);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            x[2 * q] = lo16<T>(w[q]);
-            x[2 * q + 1] = hi16<T>(w[q]);
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) x[q] = 0.f;  // (seg sums are 16-bit only: agn_wgrad rejects fp32)
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s[q] += x[q];
+  const T* lrow = sg - (ptrdiff_t)r0 * LD;  // row j of the stage at lrow + j * LD
+  auto finish = [&](float (&s)[8], int g, int end) {
+    if (end > se) {
+      if (se < rend) {  // continues in the next stage
+        *reinterpret_cast<f32x4*>(scar + f0) = f32x4{s[0], s[1], s[2], s[3]};
+        *reinterpret_cast<f32x4*>(scar + f0 + 4) = f32x4{s[4], s[5], s[6], s[7]};
+        return;
       }
-      *reinterpret_cast<uint4*>(out + (size_t)g * d.seg_ld + f0) =
-          __builtin_bit_cast(uint4, u32x4{pack2t<T>(s[0], s[1]), pack2t<T>(s[2], s[3]), pack2t<T>(s[4], s[5]),
-                                          pack2t<T>(s[6], s[7])});
+      add_rows8<T, 1>(s, G, d.ldg, se, end, f0);  // past the block's rows
     }
+    *reinterpret_cast<uint4*>(out + (size_t)g * d.seg_ld + f0) =
+        __builtin_bit_cast(uint4, u32x4{pack2t<T>(s[0], s[1]), pack2t<T>(s[2], s[3]), pack2t<T>(s[4], s[5]),
+                                        pack2t<T>(s[6], s[7])});
+  };
+  // the carried group: it ends in this stage or spans it (then no other group starts here)
+  const int gc = *gcar;
+  const int gc_end = gc >= 0 ? d.seg_ptr[gc + 1] : 0;
+  const bool carried = gc >= 0 && gc_end > r0;
+  if (carried && team == 0) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(scar + f0), b = *reinterpret_cast<const f32x4*>(scar + f0 + 4);
+    float s[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    add_rows8<T, SEG_U>(s, lrow, LD, r0, min(gc_end, se), f0);
+    finish(s, gc, gc_end);
+  }
+  const int t0 = carried ? 1 : 0, nteam = DW_THREADS / 16 - t0;
+  while (gcur < g_hi) {
+    // groups starting in this stage (in the last block's last stage also the trailing empty
+    // ones), up to 256 at once
+    const int gi = gcur + (int)threadIdx.x;
+    const bool in = gi < g_hi && (d.seg_ptr[gi] < se || se == d.rows);
+    const int cnt = __syncthreads_count(in);  // (all reads of *gcar above happen before it)
+    if (cnt == 0) break;
+    if (team >= t0)
+      for (int g = gcur + team - t0; g < gcur + cnt; g += nteam) {
+        const int beg = d.seg_ptr[g], end = d.seg_ptr[g + 1];
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        add_rows8<T, SEG_U>(s, lrow, LD, beg, min(end, se), f0);
+        if (end > se && se < rend && f0 == 0) *gcar = g;
+        finish(s, g, end);
+      }
     gcur += cnt;
     if (cnt < DW_THREADS) break;
   }
@@ -217,8 +250,8 @@ AGN_DEV int lower_bound_i32(const int32_t* ptr, int lo, int hi, int v) {
 // grid: x = row chunk (split), y = M block * nKb + K block, z = desc
 // XG: some desc has a gathered X (xidx); SEG: some desc has segment sums (seg_ptr). Separate
 // instantiations keep the plain path free of either.
-template <typename T, bool XG, bool SEG = false>
-__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
+template <typename T, bool XG, bool SEG>
+__attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b, int nsplit) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
   __shared__ __attribute__((aligned(16))) T sx[DW_ROWS * LD];
@@ -250,10 +283,12 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   // trailing empty ones); only the first output block of a split walks them
   const bool seg = SEG && d.seg_ptr && blockIdx.y == 0;
   int gcur = 0, g_hi = 0;
+  __shared__ __attribute__((aligned(16))) float scar[SEG ? DW_BLK : 1];
+  __shared__ int gcar;
   if (seg) {
     gcur = lower_bound_i32(d.seg_ptr, 0, d.seg_n, rbeg);
     g_hi = rend >= d.rows ? d.seg_n : lower_bound_i32(d.seg_ptr, gcur, d.seg_n, rend);
-    if (rbeg >= rend) seg_stage<T>(d, sg, rbeg, rbeg, gcur, g_hi, rend, true);  // an empty split's groups
+    if (threadIdx.x == 0) gcar = -1;  // (the stage loop's barriers order it)
   }
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
@@ -264,15 +299,12 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     rg.store(sg, d.g_tiled);
     rx.store(sx, d.x_tiled);
     __syncthreads();
+    if constexpr (SEG) {  // (before the next stage's loads: their registers are not live yet)
+      if (seg) seg_stage<T>(d, sg, scar, &gcar, r0, min(r0 + DW_ROWS, rend), rend, gcur, g_hi);
+    }
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
       rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, XG ? d.xidx : nullptr);
-    }
-    if constexpr (SEG) {
-      if (seg) {
-        const int stage_end = min(r0 + DW_ROWS, rend);
-        seg_stage<T>(d, sg, r0, stage_end, gcur, g_hi, stage_end, stage_end >= rend);
-      }
     }
     if (d.db_partial && kb == 0) {
       const int col = threadIdx.x & (DW_BLK - 1), q = threadIdx.x >> 7;
@@ -338,6 +370,17 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
     __syncthreads();
     if (threadIdx.x < DW_BLK) d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum + bhalf[threadIdx.x];
   }
+}
+
+template <typename T, bool XG>
+__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
+  wgrad_body<T, XG, false>(b, nsplit);
+}
+// with segment sums: held to two waves per SIMD (the walk's registers would otherwise cost the
+// occupancy the plain kernel has)
+template <typename T>
+__global__ __launch_bounds__(DW_THREADS, 2) void wgrad_seg_kernel(const agn_wgrad_batch b, int nsplit) {
+  wgrad_body<T, false, true>(b, nsplit);
 }
 
 // out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns 64 column quads (256
@@ -517,7 +560,7 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
 #define AGN_WG(T)                                                                                     \
   do {                                                                                                \
     if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns);         \
-    else if (sg) hipLaunchKernelGGL((wgrad_kernel<T, false, true>), grid, dim3(DW_THREADS), 0, st, bb, ns); \
+    else if (sg) hipLaunchKernelGGL((wgrad_seg_kernel<T>), grid, dim3(DW_THREADS), 0, st, bb, ns);       \
     else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);           \
   } while (0)
   if (dtype == AGN_BF16) AGN_WG(bf16);
