@@ -177,16 +177,24 @@ AGN_DEV void add_rows8(float (&s)[8], const T* base, size_t ld, int j0, int j1, 
 // [r0, se) of this block's range [., rend): a block owns the groups that start in its range (the
 // last block also the trailing empty ones). Each group is summed in row order from zero, as
 // agn_segment_sum does, by a 16-thread team (8 features a thread) over the stage's LDS rows; a
-// group running past the stage leaves its partial sum in LDS (scar, group id in *gcar) for team 0
-// to continue in the next stage, and one running past the block's range finishes from G in
-// memory (once per block). Every value is agn_segment_sum's bit for bit.
+// group running past the stage leaves its partial sum in LDS (SegState::car) for team 0 to
+// continue in the next stage, and one running past the block's range finishes from G in memory
+// (once per block). Every value is agn_segment_sum's bit for bit. The group bounds come from an
+// LDS window of seg_ptr (refilled every >= SEG_WIN - 256 groups), so a stage's walk waits on no
+// global load but the block's last tail.
 #ifndef AGN_SEG_U
 #define AGN_SEG_U 4
 #endif
 constexpr int SEG_U = AGN_SEG_U;  // LDS row loads in flight per walk step
+constexpr int SEG_WIN = 512;
+struct SegState {
+  float car[DW_BLK];       // the carried group's partial sum
+  int ptr[SEG_WIN + 2];    // seg_ptr[base .. base + SEG_WIN + 1] (clamped at seg_n)
+  int gc, gc_end;          // carried group (-1: none) and its end row
+};
 
 template <typename T>
-AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, float* scar, int* gcar, int r0, int se, int rend,
+AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, SegState& st, int& wbase, int r0, int se, int rend,
                        int& gcur, int g_hi) {
   constexpr int LD = DwTile<T>::LD;
   const int team = threadIdx.x >> 4, f0 = 8 * (threadIdx.x & 15);
@@ -196,8 +204,8 @@ AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, float* scar, int* g
   auto finish = [&](float (&s)[8], int g, int end) {
     if (end > se) {
       if (se < rend) {  // continues in the next stage
-        *reinterpret_cast<f32x4*>(scar + f0) = f32x4{s[0], s[1], s[2], s[3]};
-        *reinterpret_cast<f32x4*>(scar + f0 + 4) = f32x4{s[4], s[5], s[6], s[7]};
+        *reinterpret_cast<f32x4*>(st.car + f0) = f32x4{s[0], s[1], s[2], s[3]};
+        *reinterpret_cast<f32x4*>(st.car + f0 + 4) = f32x4{s[4], s[5], s[6], s[7]};
         return;
       }
       add_rows8<T, 1>(s, G, d.ldg, se, end, f0);  // past the block's rows
@@ -207,29 +215,38 @@ AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, float* scar, int* g
                                         pack2t<T>(s[6], s[7])});
   };
   // the carried group: it ends in this stage or spans it (then no other group starts here)
-  const int gc = *gcar;
-  const int gc_end = gc >= 0 ? d.seg_ptr[gc + 1] : 0;
+  const int gc = st.gc, gc_end = st.gc_end;
   const bool carried = gc >= 0 && gc_end > r0;
   if (carried && team == 0) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(scar + f0), b = *reinterpret_cast<const f32x4*>(scar + f0 + 4);
+    const f32x4 a = *reinterpret_cast<const f32x4*>(st.car + f0), b = *reinterpret_cast<const f32x4*>(st.car + f0 + 4);
     float s[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
     add_rows8<T, SEG_U>(s, lrow, LD, r0, min(gc_end, se), f0);
     finish(s, gc, gc_end);
   }
   const int t0 = carried ? 1 : 0, nteam = DW_THREADS / 16 - t0;
   while (gcur < g_hi) {
+    if (gcur + DW_THREADS > wbase + SEG_WIN) {  // (block-uniform) slide the window to gcur
+      __syncthreads();
+      wbase = gcur;
+      for (int i = threadIdx.x; i < SEG_WIN + 2; i += DW_THREADS) st.ptr[i] = d.seg_ptr[min(wbase + i, d.seg_n)];
+      __syncthreads();
+    }
+    const int* wp = st.ptr - wbase;  // wp[g] = seg_ptr[g]
     // groups starting in this stage (in the last block's last stage also the trailing empty
     // ones), up to 256 at once
     const int gi = gcur + (int)threadIdx.x;
-    const bool in = gi < g_hi && (d.seg_ptr[gi] < se || se == d.rows);
-    const int cnt = __syncthreads_count(in);  // (all reads of *gcar above happen before it)
+    const bool in = gi < g_hi && (wp[gi] < se || se == d.rows);
+    const int cnt = __syncthreads_count(in);  // (all reads of st.gc above happen before it)
     if (cnt == 0) break;
     if (team >= t0)
       for (int g = gcur + team - t0; g < gcur + cnt; g += nteam) {
-        const int beg = d.seg_ptr[g], end = d.seg_ptr[g + 1];
+        const int beg = wp[g], end = wp[g + 1];
         float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
         add_rows8<T, SEG_U>(s, lrow, LD, beg, min(end, se), f0);
-        if (end > se && se < rend && f0 == 0) *gcar = g;
+        if (end > se && se < rend && f0 == 0) {
+          st.gc = g;
+          st.gc_end = end;
+        }
         finish(s, g, end);
       }
     gcur += cnt;
@@ -283,12 +300,14 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
   // trailing empty ones); only the first output block of a split walks them
   const bool seg = SEG && d.seg_ptr && blockIdx.y == 0;
   int gcur = 0, g_hi = 0;
-  __shared__ __attribute__((aligned(16))) float scar[SEG ? DW_BLK : 1];
-  __shared__ int gcar;
-  if (seg) {
-    gcur = lower_bound_i32(d.seg_ptr, 0, d.seg_n, rbeg);
-    g_hi = rend >= d.rows ? d.seg_n : lower_bound_i32(d.seg_ptr, gcur, d.seg_n, rend);
-    if (threadIdx.x == 0) gcar = -1;  // (the stage loop's barriers order it)
+  __shared__ __attribute__((aligned(16))) std::conditional_t<SEG, SegState, char> sst;
+  int wbase = INT_MIN / 2;  // (no window yet)
+  if constexpr (SEG) {
+    if (seg) {
+      gcur = lower_bound_i32(d.seg_ptr, 0, d.seg_n, rbeg);
+      g_hi = rend >= d.rows ? d.seg_n : lower_bound_i32(d.seg_ptr, gcur, d.seg_n, rend);
+      if (threadIdx.x == 0) sst.gc = -1;  // (the stage loop's barriers order it)
+    }
   }
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
@@ -299,9 +318,6 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
     rg.store(sg, d.g_tiled);
     rx.store(sx, d.x_tiled);
     __syncthreads();
-    if constexpr (SEG) {  // (before the next stage's loads: their registers are not live yet)
-      if (seg) seg_stage<T>(d, sg, scar, &gcar, r0, min(r0 + DW_ROWS, rend), rend, gcur, g_hi);
-    }
     if (r0 + DW_ROWS < rend) {  // next stage in flight during this stage's MFMAs
       rg.load(G, d.ldg, rend, d.m, r0 + DW_ROWS, m0, d.g_tiled);
       rx.load(X, d.ldx, rend, d.k, r0 + DW_ROWS, k0, d.x_tiled, XG ? d.xidx : nullptr);
@@ -349,6 +365,9 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bb[j], acc[i][j], 0, 0, 0);
       }
+    }
+    if constexpr (SEG) {  // after the MFMAs: the walk overlaps them and the next stage's loads
+      if (seg) seg_stage<T>(d, sg, sst, wbase, r0, min(r0 + DW_ROWS, rend), rend, gcur, g_hi);
     }
   }
   // partial slab [split][mpad][kpad] with mpad = nMb*128, kpad = nKb*128
