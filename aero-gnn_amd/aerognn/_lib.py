@@ -59,8 +59,7 @@ MAX_WGRAD = 8
 class WgradDesc(C.Structure):
     _fields_ = [("g", vp), ("x", vp), ("ldg", i32), ("ldx", i32), ("m", i32), ("k", i32), ("rows", i32),
                 ("ldw", i32), ("dw_partial", vp), ("db_partial", vp), ("dw", vp), ("db", vp),
-                ("g_tiled", i32), ("x_tiled", i32), ("nsplit", i32), ("_pad", i32), ("xidx", vp),
-                ("seg_ptr", vp), ("seg_out", vp), ("seg_n", i32), ("seg_ld", i32)]
+                ("g_tiled", i32), ("x_tiled", i32), ("nsplit", i32), ("_pad", i32), ("xidx", vp)]
 
 
 class WgradBatch(C.Structure):

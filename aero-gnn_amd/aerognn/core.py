@@ -395,19 +395,12 @@ class WGrad:
     def __init__(self):
         self.items = []
 
-    def add(self, G, X, dw, db=None, xidx=None, seg=None):
-        """xidx: X is gathered, row r of the operand = X[xidx[r]] (int32, one entry per row of G).
-        seg = (rowptr, out): also out[s] = sum of G's rows rowptr[s] .. rowptr[s+1]-1 from the same
-        pass over G (segment_sum's value bit for bit; row-major 16-bit G of 128 columns)."""
+    def add(self, G, X, dw, db=None, xidx=None):
+        """xidx: X is gathered, row r of the operand = X[xidx[r]] (int32, one entry per row of G)."""
         assert G.dtype == X.dtype and logical_rows(G) == (logical_rows(X) if xidx is None else xidx.numel())
         assert dw.dtype == torch.float32 and dw.stride(1) == 1
         assert xidx is None or (xidx.dtype == torch.int32 and not is_tiled(X))
-        if seg is not None:
-            rp, out = seg
-            assert xidx is None and not is_tiled(G) and G.shape[1] == 128 and G.dtype != torch.float32
-            assert rp.dtype == torch.int32 and out.dtype == G.dtype and out.shape[0] == rp.numel() - 1
-            assert out.stride(1) == 1 and out.shape[1] == 128
-        self.items.append((G, X, dw, db, xidx, seg))
+        self.items.append((G, X, dw, db, xidx))
 
     def run(self):
         lib = L.lib()
@@ -420,32 +413,29 @@ class WGrad:
         for chunk in chunks:
             dev = chunk[0][0].device
             live = []
-            for G, X, dw, db, xi, sg in chunk:
+            for G, X, dw, db, xi in chunk:
                 if logical_rows(G) == 0:
                     dw.zero_()
                     if db is not None:
                         db.zero_()
-                    if sg is not None:
-                        sg[1].zero_()
                 else:
-                    live.append((G, X, dw, db, xi, sg))
+                    live.append((G, X, dw, db, xi))
             if not live:
                 continue
             b = L.WgradBatch()
             b.n = len(live)
-            for j, (G, X, dw, db, xi, sg) in enumerate(live):
+            for j, (G, X, dw, db, xi) in enumerate(live):
                 b.d[j] = L.WgradDesc(ptr(G), ptr(X), G.stride(0), X.stride(0), G.shape[1], X.shape[1], logical_rows(G),
                                      dw.stride(0), None, None, ptr(dw), ptr(db), int(is_tiled(G)), int(is_tiled(X)), 0, 0,
-                                     ptr(xi), ptr(sg[0]) if sg else None, ptr(sg[1]) if sg else None,
-                                     sg[1].shape[0] if sg else 0, sg[1].stride(0) if sg else 0)
+                                     ptr(xi))
             check(lib.agn_wgrad_plan(C.byref(b)), "wgrad_plan")  # one uniform split count, from the largest desc
             sizes = [int(lib.agn_wgrad_partial_floats(G.shape[1], X.shape[1], b.d[j].nsplit))
-                     for j, (G, X, _, _, _, _) in enumerate(live)]
+                     for j, (G, X, _, _, _) in enumerate(live)]
             bsz = [b.d[j].nsplit * ((G.shape[1] + 127) // 128) * 128 if db is not None else 0
-                   for j, (G, _, _, db, _, _) in enumerate(live)]
+                   for j, (G, _, _, db, _) in enumerate(live)]
             scratch = torch.empty(sum(sizes) + sum(bsz), dtype=torch.float32, device=dev)
             o = 0
-            for j, (G, X, dw, db, _, _) in enumerate(live):
+            for j, (G, X, dw, db, _) in enumerate(live):
                 b.d[j].dw_partial = ptr(scratch[o:o + sizes[j]])
                 o += sizes[j]
                 if db is not None:
@@ -455,8 +445,8 @@ class WGrad:
             # share is 0 (a fused backward keeps G in registers), so the alg_bytes slot carries 0
             s_el = live[0][0].element_size()
             io = sum(logical_rows(G) * (G.shape[1] + X.shape[1]) * s_el + 4 * G.shape[1] * (X.shape[1] + 1)
-                     for G, X, _, _, _, _ in live)
-            fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _, _, _ in live)
+                     for G, X, _, _, _ in live)
+            fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _, _ in live)
             with timed("wgrad", (0.0, fl, io)):
                 check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
         self.items = []

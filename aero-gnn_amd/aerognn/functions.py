@@ -16,7 +16,6 @@ gradients are G^T X products accumulated in fp32.
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
@@ -28,11 +27,6 @@ from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
                    timed, gather_rows, mlp_backward, mlp_forward, require_device,
                    scatter_rows, segment_max, segment_max_backward, segment_sum, segment_sum2, stream)
-
-
-# the fused sum-trick backward takes dP_d from the dW_e pass (agn_wgrad seg_*); 0 = a separate
-# segment_sum launch (same values bit for bit: A/B timing only)
-WGRAD_SEG = os.environ.get("AEROGNN_WGRAD_SEG", "1") != "0"
 
 
 def _c(t):
@@ -504,21 +498,7 @@ class GMPFn(torch.autograd.Function):
         if spec.trick:
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
             dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
-            dPd = torch.empty(N, H, dtype=dt, device=dev)
-            if fused and WGRAD_SEG:
-                # dW_e = G0^T e, with the receiver sums dP_d of G0 (edges are receiver-sorted, so the
-                # groups are contiguous row ranges) from the same pass over G0
-                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
-                we = WGrad()
-                we.add(g0, e, dwe, seg=(lv.rowptr, dPd))
-                we.run()
-            else:
-                segment_sum(N, H, lv.rowptr, None, g0, dPd)
-                if fused:
-                    dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
-                    we = WGrad()
-                    we.add(g0, e, dwe)
-                    we.run()
+            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
             if proj_kernel_ok(dx, H):
                 s_el = dx.element_size()
                 proj_backward(N, dPs, dPd, spec.pack["projT"], dx, tag="proj_bwd",
@@ -533,6 +513,10 @@ class GMPFn(torch.autograd.Function):
             # different row counts leaves most workgroups idle behind the edge descs (measured)
             wg = WGrad()
             if fused:
+                dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
+                we = WGrad()
+                we.add(g0, e, dwe)
+                we.run()
                 eg = [dwe]
                 for l in range(3):
                     eg += [dW13[l], db13[l]]

@@ -156,119 +156,10 @@ AGN_DEV bf16x8 tr_frag(const bf16* lds, int kb, int col_base, int lane) {
   return r;
 }
 
-// rows j0 .. j1-1 (8 features from f0) added in order into s
-template <typename T, int U>
-AGN_DEV void add_rows8(float (&s)[8], const T* base, size_t ld, int j0, int j1, int f0) {
-#pragma unroll U
-  for (int j = j0; j < j1; ++j) {
-    const u32x4 w = __builtin_bit_cast(u32x4, *reinterpret_cast<const uint4*>(base + (size_t)j * ld + f0));
-    float x[8];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      x[2 * q] = lo16<T>(w[q]);
-      x[2 * q + 1] = hi16<T>(w[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s[q] += x[q];
-  }
-}
-
-// Segment sums of G's rows (agn_wgrad_desc.seg_*), 16-bit G only, from the staged rows
-// [r0, se) of this block's range [., rend): a block owns the groups that start in its range (the
-// last block also the trailing empty ones). Each group is summed in row order from zero, as
-// agn_segment_sum does, by a 16-thread team (8 features a thread) over the stage's LDS rows; a
-// group running past the stage leaves its partial sum in LDS (SegState::car) for team 0 to
-// continue in the next stage, and one running past the block's range finishes from G in memory
-// (once per block). Every value is agn_segment_sum's bit for bit. The group bounds come from an
-// LDS window of seg_ptr (refilled every >= SEG_WIN - 256 groups), so a stage's walk waits on no
-// global load but the block's last tail.
-#ifndef AGN_SEG_U
-#define AGN_SEG_U 4
-#endif
-constexpr int SEG_U = AGN_SEG_U;  // LDS row loads in flight per walk step
-constexpr int SEG_WIN = 512;
-struct SegState {
-  float car[DW_BLK];       // the carried group's partial sum
-  int ptr[SEG_WIN + 2];    // seg_ptr[base .. base + SEG_WIN + 1] (clamped at seg_n)
-  int gc, gc_end;          // carried group (-1: none) and its end row
-};
-
-template <typename T>
-AGN_DEV void seg_stage(const agn_wgrad_desc& d, const T* sg, SegState& st, int& wbase, int r0, int se, int rend,
-                       int& gcur, int g_hi) {
-  constexpr int LD = DwTile<T>::LD;
-  const int team = threadIdx.x >> 4, f0 = 8 * (threadIdx.x & 15);
-  const T* G = reinterpret_cast<const T*>(d.g);
-  T* out = reinterpret_cast<T*>(d.seg_out);
-  const T* lrow = sg - (ptrdiff_t)r0 * LD;  // row j of the stage at lrow + j * LD
-  auto finish = [&](float (&s)[8], int g, int end) {
-    if (end > se) {
-      if (se < rend) {  // continues in the next stage
-        *reinterpret_cast<f32x4*>(st.car + f0) = f32x4{s[0], s[1], s[2], s[3]};
-        *reinterpret_cast<f32x4*>(st.car + f0 + 4) = f32x4{s[4], s[5], s[6], s[7]};
-        return;
-      }
-      add_rows8<T, 1>(s, G, d.ldg, se, end, f0);  // past the block's rows
-    }
-    *reinterpret_cast<uint4*>(out + (size_t)g * d.seg_ld + f0) =
-        __builtin_bit_cast(uint4, u32x4{pack2t<T>(s[0], s[1]), pack2t<T>(s[2], s[3]), pack2t<T>(s[4], s[5]),
-                                        pack2t<T>(s[6], s[7])});
-  };
-  // the carried group: it ends in this stage or spans it (then no other group starts here)
-  const int gc = st.gc, gc_end = st.gc_end;
-  const bool carried = gc >= 0 && gc_end > r0;
-  if (carried && team == 0) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(st.car + f0), b = *reinterpret_cast<const f32x4*>(st.car + f0 + 4);
-    float s[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-    add_rows8<T, SEG_U>(s, lrow, LD, r0, min(gc_end, se), f0);
-    finish(s, gc, gc_end);
-  }
-  const int t0 = carried ? 1 : 0, nteam = DW_THREADS / 16 - t0;
-  while (gcur < g_hi) {
-    if (gcur + DW_THREADS > wbase + SEG_WIN) {  // (block-uniform) slide the window to gcur
-      __syncthreads();
-      wbase = gcur;
-      for (int i = threadIdx.x; i < SEG_WIN + 2; i += DW_THREADS) st.ptr[i] = d.seg_ptr[min(wbase + i, d.seg_n)];
-      __syncthreads();
-    }
-    const int* wp = st.ptr - wbase;  // wp[g] = seg_ptr[g]
-    // groups starting in this stage (in the last block's last stage also the trailing empty
-    // ones), up to 256 at once
-    const int gi = gcur + (int)threadIdx.x;
-    const bool in = gi < g_hi && (wp[gi] < se || se == d.rows);
-    const int cnt = __syncthreads_count(in);  // (all reads of st.gc above happen before it)
-    if (cnt == 0) break;
-    if (team >= t0)
-      for (int g = gcur + team - t0; g < gcur + cnt; g += nteam) {
-        const int beg = wp[g], end = wp[g + 1];
-        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        add_rows8<T, SEG_U>(s, lrow, LD, beg, min(end, se), f0);
-        if (end > se && se < rend && f0 == 0) {
-          st.gc = g;
-          st.gc_end = end;
-        }
-        finish(s, g, end);
-      }
-    gcur += cnt;
-    if (cnt < DW_THREADS) break;
-  }
-}
-
-// first index g in [lo, hi) with ptr[g] >= v (hi if none); ptr non-decreasing
-AGN_DEV int lower_bound_i32(const int32_t* ptr, int lo, int hi, int v) {
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (ptr[mid] < v) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
 // grid: x = row chunk (split), y = M block * nKb + K block, z = desc
-// XG: some desc has a gathered X (xidx); SEG: some desc has segment sums (seg_ptr). Separate
-// instantiations keep the plain path free of either.
-template <typename T, bool XG, bool SEG>
-__attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b, int nsplit) {
+// XG: some desc has a gathered X (xidx); a separate instantiation keeps the plain path free of it
+template <typename T, bool XG>
+__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
   constexpr int LD = DwTile<T>::LD;
   __shared__ __attribute__((aligned(16))) T sg[DW_ROWS * LD];
   __shared__ __attribute__((aligned(16))) T sx[DW_ROWS * LD];
@@ -296,19 +187,6 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
   float bsum = 0.f;
   __shared__ float bhalf[DW_BLK];
   StageRegs<T> rg, rx;
-  // segment sums: this block owns the groups starting in [rbeg, rend) (and, ending the rows, the
-  // trailing empty ones); only the first output block of a split walks them
-  const bool seg = SEG && d.seg_ptr && blockIdx.y == 0;
-  int gcur = 0, g_hi = 0;
-  __shared__ __attribute__((aligned(16))) std::conditional_t<SEG, SegState, char> sst;
-  int wbase = INT_MIN / 2;  // (no window yet)
-  if constexpr (SEG) {
-    if (seg) {
-      gcur = lower_bound_i32(d.seg_ptr, 0, d.seg_n, rbeg);
-      g_hi = rend >= d.rows ? d.seg_n : lower_bound_i32(d.seg_ptr, gcur, d.seg_n, rend);
-      if (threadIdx.x == 0) sst.gc = -1;  // (the stage loop's barriers order it)
-    }
-  }
   if (rbeg < rend) {
     rg.load(G, d.ldg, rend, d.m, rbeg, m0, d.g_tiled);
     rx.load(X, d.ldx, rend, d.k, rbeg, k0, d.x_tiled, XG ? d.xidx : nullptr);
@@ -366,9 +244,6 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], bb[j], acc[i][j], 0, 0, 0);
       }
     }
-    if constexpr (SEG) {  // after the MFMAs: the walk overlaps them and the next stage's loads
-      if (seg) seg_stage<T>(d, sg, sst, wbase, r0, min(r0 + DW_ROWS, rend), rend, gcur, g_hi);
-    }
   }
   // partial slab [split][mpad][kpad] with mpad = nMb*128, kpad = nKb*128
   const int kpad = nKb * DW_BLK;
@@ -389,17 +264,6 @@ __attribute__((always_inline)) AGN_DEV void wgrad_body(const agn_wgrad_batch& b,
     __syncthreads();
     if (threadIdx.x < DW_BLK) d.db_partial[(size_t)split * (nMb * DW_BLK) + m0 + threadIdx.x] = bsum + bhalf[threadIdx.x];
   }
-}
-
-template <typename T, bool XG>
-__global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch b, int nsplit) {
-  wgrad_body<T, XG, false>(b, nsplit);
-}
-// with segment sums: held to two waves per SIMD (the walk's registers would otherwise cost the
-// occupancy the plain kernel has)
-template <typename T>
-__global__ __launch_bounds__(DW_THREADS, 2) void wgrad_seg_kernel(const agn_wgrad_batch b, int nsplit) {
-  wgrad_body<T, false, true>(b, nsplit);
 }
 
 // out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns 64 column quads (256
@@ -565,29 +429,17 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   }
   (void)total;
   dim3 grid(ns, maxblk, bb.n);
-  bool xg = false, sg = false;
-  for (int i = 0; i < bb.n; ++i) {
-    xg = xg || bb.d[i].xidx != nullptr;
-    if (bb.d[i].seg_ptr) {
-      if (bb.d[i].g_tiled || bb.d[i].m != DW_BLK || !bb.d[i].seg_out || bb.d[i].seg_n < 0 || bb.d[i].seg_ld < DW_BLK ||
-          bb.d[i].seg_ld % 8 || dtype == AGN_F32)
-        return AGN_E_ARG;
-      sg = true;
-    }
-  }
-  if (xg && sg) return AGN_E_ARG;  // one special instantiation per launch
-#define AGN_WG(T)                                                                                     \
-  do {                                                                                                \
-    if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns);         \
-    else if (sg) hipLaunchKernelGGL((wgrad_seg_kernel<T>), grid, dim3(DW_THREADS), 0, st, bb, ns);       \
-    else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);           \
+  bool xg = false;
+  for (int i = 0; i < bb.n; ++i) xg = xg || bb.d[i].xidx != nullptr;
+#define AGN_WG(T)                                                                             \
+  do {                                                                                        \
+    if (xg) hipLaunchKernelGGL((wgrad_kernel<T, true>), grid, dim3(DW_THREADS), 0, st, bb, ns); \
+    else hipLaunchKernelGGL((wgrad_kernel<T, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);   \
   } while (0)
   if (dtype == AGN_BF16) AGN_WG(bf16);
   else if (dtype == AGN_F16) AGN_WG(f16);
-  else if (dtype == AGN_F32) {  // (no segment sums in fp32: rejected above)
-    if (xg) hipLaunchKernelGGL((wgrad_kernel<float, true>), grid, dim3(DW_THREADS), 0, st, bb, ns);
-    else hipLaunchKernelGGL((wgrad_kernel<float, false>), grid, dim3(DW_THREADS), 0, st, bb, ns);
-  } else return AGN_E_DTYPE;
+  else if (dtype == AGN_F32) AGN_WG(float);
+  else return AGN_E_DTYPE;
 #undef AGN_WG
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
   return launch_status();

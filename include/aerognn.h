@@ -167,13 +167,6 @@ typedef struct {
   const int32_t* xidx;  /* NULL, or a gathered X: logical row r is x's row xidx[r] (x[src] / x[dst]
                            of the concat edge MLP, mgnLayer.py:10-49, without an [E][k] copy);
                            row-major x only (x_tiled == 0) */
-  /* optional segment sums of G over row groups, from the same pass over G (the sum-trick edge
-   * block's dP_d = receiver sums of G0 beside dW_e = G0^T e, mgnLayer.py:97-103): seg_out[s] =
-   * sum of G's rows seg_ptr[s] .. seg_ptr[s+1]-1 in row order in fp32, rounded once to G's dtype
-   * (agn_segment_sum's value bit for bit), s < seg_n; seg_ptr NULL = none. Row-major G, m = 128. */
-  const int32_t* seg_ptr;
-  void* seg_out;
-  int seg_n, seg_ld;
 } agn_wgrad_desc;
 typedef struct {
   int n;

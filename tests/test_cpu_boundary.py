@@ -34,8 +34,7 @@ def test_struct_layouts_match_c(tmp_path):
               "agn_mlp_fwd_args": (L.MlpFwdArgs, ["seg", "wpk", "bias", "ln_g", "proj", "resid", "act", "stats", "mask"]),
               "agn_mlp_bwd_args": (L.MlpBwdArgs, ["wtpk", "act", "g", "gidx", "gpre", "din_nseg", "din_k", "din",
                                                  "din_resid", "ln_partial"]),
-              "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db", "nsplit", "xidx", "seg_ptr",
-                                                "seg_out", "seg_n", "seg_ld"]),
+              "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db", "nsplit", "xidx"]),
               "agn_wgrad_batch": (L.WgradBatch, ["n", "d"]),
               "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")]),
               "agn_edge_bwd_args": (L.EdgeBwdArgs, [f for f, _ in L.EdgeBwdArgs._fields_])}

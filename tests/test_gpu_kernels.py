@@ -68,43 +68,6 @@ def test_wgrad_gathered_operand(dtype, rows, N, K):
     assert rel_l2(dw, ref) <= 1e-6 and rel_l2(db, G.double().sum(0)) <= 1e-6
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("rows,N,kind", [(1, 1, "plain"), (5000, 300, "plain"), (70001, 3000, "ragged"),
-                                          (40000, 7, "long"), (3000, 5000, "sparse")])
-def test_wgrad_segment_sums_equal_segment_sum(dtype, rows, N, kind):
-    """agn_wgrad's seg_*: the receiver sums of G from the dW pass (the sum-trick backward's dP_d)
-    equal agn_segment_sum bit for bit - groups crossing stage and split boundaries, empty groups at
-    the front, middle and end, groups longer than a stage - and dW / db are unchanged by them."""
-    from aerognn.core import WGrad, segment_sum
-    g = torch.Generator(device="cpu").manual_seed(rows + N)
-    G = torch.randn(rows, 128, generator=g).to(DEV, dtype)
-    X = torch.randn(rows, 128, generator=g).to(DEV, dtype)
-    if kind == "long":  # few receivers: every group spans many stages and splits
-        recv = torch.randint(1, N - 1, (rows,), generator=g)
-    elif kind == "sparse":  # more receivers than rows: mostly empty groups
-        recv = torch.randint(0, N, (rows,), generator=g)
-    elif kind == "ragged":  # a heavy-tailed degree mix
-        recv = (torch.rand(rows, generator=g) ** 3 * N).long().clamp_max(N - 1)
-    else:
-        recv = torch.randint(0, N, (rows,), generator=g)
-    cnt = torch.bincount(recv, minlength=N)
-    rp = torch.zeros(N + 1, dtype=torch.int64)
-    rp[1:] = torch.cumsum(cnt, 0)
-    rp = rp.to(torch.int32).to(DEV)
-    seg = torch.full((N, 128), float("nan"), dtype=dtype, device=DEV)
-    dw, db = (torch.empty(128, 128, dtype=torch.float32, device=DEV) for _ in range(2))
-    db = db[0]
-    dw2, db2 = torch.empty_like(dw), torch.empty_like(db)
-    wg = WGrad()
-    wg.add(G, X, dw, db, seg=(rp, seg))
-    wg.run()
-    wg.add(G, X, dw2, db2)
-    wg.run()
-    ref = segment_sum(N, 128, rp, None, G, torch.empty(N, 128, dtype=dtype, device=DEV))
-    assert torch.equal(seg, ref)
-    assert torch.equal(dw, dw2) and torch.equal(db, db2)
-
-
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_base", [True, False])
 def test_segment_sum2_vs_torch(dtype, with_base):
