@@ -99,8 +99,6 @@ def test_segment_sum2_vs_torch(dtype, with_base):
     assert rel_l2(out.cpu(), ref) <= tol
     if dtype == torch.float32:
         assert torch.equal(out, comp)
-    if dtype == torch.float32:
-        assert torch.equal(out, comp)
 
 
 @pytest.mark.parametrize("nw,n", [(1, 256), (47000, 256), (5, 7)])
