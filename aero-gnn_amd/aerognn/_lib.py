@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("AEROGNN_LIB") or os.path.join(_HERE, "libaerognn.so")
 
 MAX_LIN = 8
 MAX_SEG = 3
-F32, BF16, F16 = 0, 1, 2
+F32, BF16, F16, F64 = 0, 1, 2, 3
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
 OPT_RESIDENT = 0
 
@@ -85,6 +85,22 @@ class PackDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
                 ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
                 ("row_off", i32), ("col_off", i32), ("dst_rows", i32), ("dst_cols", i32)]
+
+
+class F64Seg(C.Structure):
+    _fields_ = [("a", vp), ("aidx", vp), ("lda", i32), ("k", i32), ("w", vp), ("ldw", i32), ("transw", i32)]
+
+
+class F64GemmArgs(C.Structure):
+    _fields_ = [("rows", i32), ("n", i32), ("nseg", i32), ("_pad", i32), ("seg", F64Seg * 3), ("bias", vp),
+                ("add", vp * 2), ("add_idx", vp * 2), ("add_ld", i32 * 2), ("mask", vp), ("mask_ld", i32),
+                ("relu", i32), ("out", vp), ("out_ld", i32), ("_pad2", i32)]
+
+
+class F64WgradArgs(C.Structure):
+    _fields_ = [("rows", i32), ("m", i32), ("k", i32), ("_pad", i32), ("g", vp), ("ldg", i32), ("_pad1", i32),
+                ("x", vp), ("ldx", i32), ("_pad2", i32), ("xidx", vp), ("dw", vp), ("ldw", i32), ("_pad3", i32),
+                ("db", vp)]
 
 
 _lib = None
@@ -204,6 +220,12 @@ def lib():
             "agn_proj_backward": (i32, [i32, vp, vp, i32, vp, vp, i32, vp]),
             "agn_wec_forward": (i32, [C.POINTER(WecArgs), vp]),
             "agn_wec_backward": (i32, [C.POINTER(WecArgs), vp]),
+            "agn_f64_gemm": (i32, [C.POINTER(F64GemmArgs), vp]),
+            "agn_f64_wgrad_scratch_bytes": (C.c_size_t, [C.POINTER(F64WgradArgs)]),
+            "agn_f64_wgrad": (i32, [C.POINTER(F64WgradArgs), vp, vp]),
+            "agn_f64_layernorm_fwd": (i32, [i32, i32, vp, i32, vp, vp, vp, i32, vp, i32, vp, vp, C.c_double, vp]),
+            "agn_f64_layernorm_bwd_scratch_bytes": (C.c_size_t, [i32, i32]),
+            "agn_f64_layernorm_bwd": (i32, [i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, i32, vp, vp, vp, vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

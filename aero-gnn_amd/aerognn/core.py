@@ -62,7 +62,9 @@ def dt_code(dtype) -> int:
         return L.BF16
     if dtype == torch.float16:
         return L.F16
-    raise NotImplementedError(f"aerognn kernels compute in float32, bfloat16 or float16, got {dtype}")
+    if dtype == torch.float64:  # graph ops and the agn_f64_* kernels (aerognn/f64.py)
+        return L.F64
+    raise NotImplementedError(f"aerognn kernels compute in float64, float32, bfloat16 or float16, got {dtype}")
 
 
 def tiled_empty(rows, width, dtype, device):

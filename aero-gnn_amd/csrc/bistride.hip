@@ -551,6 +551,9 @@ int agn_scatter_rows(int rows, int k, int dtype, const int32_t* idx, const void*
   else if (dtype == AGN_F16)
     hipLaunchKernelGGL(scatter_rows_kernel<f16>, g, dim3(256), 0, st, rows, k, idx, (const f16*)src, src_ld,
                        (f16*)out, out_ld);
+  else if (dtype == AGN_F64)
+    hipLaunchKernelGGL(scatter_rows_kernel<double>, g, dim3(256), 0, st, rows, k, idx, (const double*)src, src_ld,
+                       (double*)out, out_ld);
   else
     return AGN_E_DTYPE;
   return launch_status();

@@ -53,6 +53,48 @@ AGN_DEV void store8(T* row, int f0, int k, bool vec, const float (&v)[8]) {
     if (f0 + i < k) row[f0 + i] = from_f<T>(v[i]);
 }
 
+// float64 (train.py's "double" precision, train.py:20-40): the same kernels with double
+// accumulators; 16-, 32-bit storage accumulates in fp32 as above.
+template <typename T> struct AccOf { using type = float; };
+template <> struct AccOf<double> { using type = double; };
+template <typename T> using acc_of = typename AccOf<T>::type;
+template <typename T> AGN_DEV acc_of<T> ld1(T v) {
+  if constexpr (std::is_same<T, double>::value) return v;
+  else return to_f(v);
+}
+template <typename T> AGN_DEV T st1(acc_of<T> v) {
+  if constexpr (std::is_same<T, double>::value) return v;
+  else return from_f<T>(v);
+}
+template <typename T> AGN_DEV acc_of<T> rnd(acc_of<T> v) {
+  if constexpr (std::is_same<T, double>::value) return v;
+  else return round_t<T>(v);
+}
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+AGN_DEV void load8(double (&o)[8], const double* row, int f0, int k, bool vec) {
+  if (vec && f0 + 7 < k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f64x2 x = *reinterpret_cast<const f64x2*>(row + f0 + 2 * i);
+      o[2 * i] = x[0];
+      o[2 * i + 1] = x[1];
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (f0 + i < k) ? row[f0 + i] : 0.0;
+}
+AGN_DEV void store8(double* row, int f0, int k, bool vec, const double (&v)[8]) {
+  if (vec && f0 + 7 < k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f64x2*>(row + f0 + 2 * i) = f64x2{v[2 * i], v[2 * i + 1]};
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (f0 + i < k) row[f0 + i] = v[i];
+}
+
 // out[r] = sum_{j in ptr[r]..ptr[r+1]-1} src[perm ? perm[j] : j]   (/ max(count,1) if mean)
 // 16 threads per row, 8 features (16 B of bf16) per thread per pass; fp32 accumulation in
 // index order (two rows' loads in flight per step, summed in order).
@@ -68,12 +110,13 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   constexpr int A = 16 / sizeof(T);
   const bool vec = ((k % A) == 0) && ((src_ld % A) == 0) && ((out_ld % A) == 0) &&
                    ((((uintptr_t)src) | ((uintptr_t)out)) & 15) == 0;
+  using A_t = acc_of<T>;
   for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    A_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int j = beg;
     for (; j + 1 < end; j += 2) {
       const int e0 = perm ? perm[j] : j, e1 = perm ? perm[j + 1] : j + 1;
-      float x[8], y[8];
+      A_t x[8], y[8];
       load8(x, src + (size_t)e0 * src_ld, f0, k, vec);
       load8(y, src + (size_t)e1 * src_ld, f0, k, vec);
 #pragma unroll
@@ -81,13 +124,13 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
     }
     if (j < end) {
       const int e0 = perm ? perm[j] : j;
-      float x[8];
+      A_t x[8];
       load8(x, src + (size_t)e0 * src_ld, f0, k, vec);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] += x[i];
     }
     if (mean) {
-      const float cnt = (float)max(end - beg, 1);
+      const A_t cnt = (A_t)max(end - beg, 1);
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] /= cnt;
     }
@@ -98,12 +141,12 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
 // out[r] = (base[r] + (group a of r)) + (group b of r): the concat edge MLP's node gradient in one
 // pass (agn_segment_sum2). Same thread layout and in-order fp32 accumulation as segment_sum_kernel.
 template <typename T>
-AGN_DEV void seg_accum(float (&s)[8], int beg, int end, const int32_t* __restrict__ perm, const T* __restrict__ src,
+AGN_DEV void seg_accum(acc_of<T> (&s)[8], int beg, int end, const int32_t* __restrict__ perm, const T* __restrict__ src,
                        int ld, int f0, int k, bool vec) {
   int j = beg;
   for (; j + 1 < end; j += 2) {
     const int e0 = perm ? perm[j] : j, e1 = perm ? perm[j + 1] : j + 1;
-    float x[8], y[8];
+    acc_of<T> x[8], y[8];
     load8(x, src + (size_t)e0 * ld, f0, k, vec);
     load8(y, src + (size_t)e1 * ld, f0, k, vec);
 #pragma unroll
@@ -111,7 +154,7 @@ AGN_DEV void seg_accum(float (&s)[8], int beg, int end, const int32_t* __restric
   }
   if (j < end) {
     const int e0 = perm ? perm[j] : j;
-    float x[8];
+    acc_of<T> x[8];
     load8(x, src + (size_t)e0 * ld, f0, k, vec);
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] += x[i];
@@ -136,10 +179,10 @@ __global__ __launch_bounds__(256) void segment_sum2_kernel(int rows, int k, cons
   for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
     // each group summed from zero in edge order (segment_sum_kernel's sums), then
     // (base + sum_a) + sum_b: in fp32 bitwise the two-segment-sum composition it replaces
-    float sa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, sb[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    acc_of<T> sa[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     seg_accum(sa, ptr_a[r], ptr_a[r + 1], perm_a, src_a, lda, f0, k, vec);
     seg_accum(sb, ptr_b[r], ptr_b[r + 1], perm_b, src_b, ldb, f0, k, vec);
-    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    acc_of<T> s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (base) load8(s, base + (size_t)r * base_ld, f0, k, vec);  // read before this thread's own store (out may alias)
 #pragma unroll
     for (int i = 0; i < 8; ++i) s[i] = base ? (s[i] + sa[i]) + sb[i] : sa[i] + sb[i];
@@ -161,14 +204,14 @@ __global__ __launch_bounds__(256) void segment_max_kernel(int rows, int k, const
   if (t >= (long)rows * k) return;
   const int r = (int)(t / k), f = (int)(t - (long)r * k);
   const int beg = ptr[r], end = ptr[r + 1];
-  float best = 0.f;
+  acc_of<T> best = 0;
   int arg = -1;
   for (int j = beg; j < end; ++j) {
     const int e = perm ? perm[j] : j;
-    const float v = to_f(src[(size_t)e * src_ld + f]);
+    const acc_of<T> v = ld1<T>(src[(size_t)e * src_ld + f]);
     if (arg < 0 || v > best || (v != v && best == best)) { best = v; arg = e; }
   }
-  out[(size_t)r * out_ld + f] = from_f<T>(best);
+  out[(size_t)r * out_ld + f] = st1<T>(best);
   argmax[(size_t)r * k + f] = arg;
 }
 
@@ -199,10 +242,11 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const
   constexpr int A = 16 / sizeof(T);
   const bool vec = ((k % A) == 0) && ((src_ld % A) == 0) && ((out_ld % A) == 0) && ((add_ld % A) == 0) &&
                    ((((uintptr_t)src) | ((uintptr_t)out) | ((uintptr_t)add)) & 15) == 0;
-  float div = 1.f;
-  if (cnt_ptr) div = (float)max(cnt_ptr[s + 1] - cnt_ptr[s], 1);
+  using A_t = acc_of<T>;
+  A_t div = 1;
+  if (cnt_ptr) div = (A_t)max(cnt_ptr[s + 1] - cnt_ptr[s], 1);
   for (int f0 = 8 * sub; f0 < k; f0 += 8 * SEG_TPR) {
-    float x[8];
+    A_t x[8];
     load8(x, src + (size_t)s * src_ld, f0, k, vec);
     if (cnt_ptr) {
 #pragma unroll
@@ -210,10 +254,10 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const
     }
     if (add) {
       // the reference rounds the gathered value to T before the add (bsms_mgn.py:199-200)
-      float y[8];
+      A_t y[8];
       load8(y, add + (size_t)r * add_ld, f0, k, vec);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = round_t<T>(x[i]) + y[i];
+      for (int i = 0; i < 8; ++i) x[i] = rnd<T>(x[i]) + y[i];
     }
     store8(out + (size_t)r * out_ld, f0, k, vec, x);
   }
@@ -680,6 +724,7 @@ int agn_segment_sum(int rows, int k, int dtype, const int32_t* ptr, const int32_
   if (dtype == AGN_F32) return seg_sum_t<float>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_BF16) return seg_sum_t<bf16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   if (dtype == AGN_F16) return seg_sum_t<f16>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
+  if (dtype == AGN_F64) return seg_sum_t<double>(rows, k, ptr, perm, src, src_ld, out, out_ld, mean, st);
   return AGN_E_DTYPE;
 }
 
@@ -694,6 +739,7 @@ int agn_segment_sum2(int rows, int k, int dtype, const void* base, int base_ld, 
   if (dtype == AGN_F32) return AGN_SS2(float);
   if (dtype == AGN_BF16) return AGN_SS2(bf16);
   if (dtype == AGN_F16) return AGN_SS2(f16);
+  if (dtype == AGN_F64) return AGN_SS2(double);
 #undef AGN_SS2
   return AGN_E_DTYPE;
 }
@@ -714,6 +760,9 @@ int agn_segment_max(int rows, int k, int dtype, const int32_t* ptr, const int32_
   else if (dtype == AGN_F16)
     hipLaunchKernelGGL(segment_max_kernel<f16>, g, dim3(256), 0, st, rows, k, ptr, perm, (const f16*)src, src_ld,
                        (f16*)out, out_ld, argmax);
+  else if (dtype == AGN_F64)
+    hipLaunchKernelGGL(segment_max_kernel<double>, g, dim3(256), 0, st, rows, k, ptr, perm, (const double*)src, src_ld,
+                       (double*)out, out_ld, argmax);
   else
     return AGN_E_DTYPE;
   const hipError_t e = hipGetLastError();
@@ -736,6 +785,9 @@ int agn_segment_max_backward(int rows, int k, int dtype, const int32_t* argmax, 
   else if (dtype == AGN_F16)
     hipLaunchKernelGGL(segment_max_bwd_kernel<f16>, g, dim3(256), 0, st, rows, k, argmax, (const f16*)gout, gout_ld,
                        (f16*)dx, dx_ld);
+  else if (dtype == AGN_F64)
+    hipLaunchKernelGGL(segment_max_bwd_kernel<double>, g, dim3(256), 0, st, rows, k, argmax, (const double*)gout,
+                       gout_ld, (double*)dx, dx_ld);
   else
     return AGN_E_DTYPE;
   const hipError_t e = hipGetLastError();
@@ -750,6 +802,7 @@ int agn_gather_rows(int rows, int k, int dtype, const int32_t* idx, const void* 
   if (dtype == AGN_F32) return gather_t<float>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
   if (dtype == AGN_BF16) return gather_t<bf16>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
   if (dtype == AGN_F16) return gather_t<f16>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
+  if (dtype == AGN_F64) return gather_t<double>(rows, k, idx, src, src_ld, cnt_ptr, add, add_ld, out, out_ld, st);
   return AGN_E_DTYPE;
 }
 

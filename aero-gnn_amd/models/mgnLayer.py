@@ -11,6 +11,7 @@ import os
 import torch
 from torch import nn
 
+from aerognn import f64
 from aerognn.functions import EdgeBlockFn, GMPFn, LayerSpec, NodeBlockFn, from_csc, to_csc
 from aerognn.graph import Level
 from models.mlp import MLP
@@ -38,8 +39,10 @@ class EdgeBlock(nn.Module):
         return self._spec
 
     def forward(self, edge_attr, node_attr, edge_index):
-        s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
+        if node_attr.dtype == torch.float64:  # train.py precision "double" (aerognn/f64.py)
+            return from_csc(f64.edge_update(self, node_attr, to_csc(edge_attr, lv), lv), lv)
+        s = self.spec()
         s.pack.update(node_attr.dtype, node_attr.device)
         out = EdgeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.edge_params())
         return from_csc(out, lv)
@@ -81,8 +84,10 @@ class EdgeBlockSum(nn.Module):
         return self._spec
 
     def forward(self, edge_attr, node_attr, edge_index):
-        s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
+        if node_attr.dtype == torch.float64:  # train.py precision "double" (aerognn/f64.py)
+            return from_csc(f64.edge_update(self, node_attr, to_csc(edge_attr, lv), lv), lv)
+        s = self.spec()
         s.pack.update(node_attr.dtype, node_attr.device)
         out = EdgeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.edge_params())
         return from_csc(out, lv)
@@ -109,8 +114,10 @@ class NodeBlock(nn.Module):
     def forward(self, node_attr, edge_attr, edge_index):
         if self.aggregation not in ('mean', 'add'):
             raise ValueError(f"Unsupported aggregation method: {self.aggregation}")
-        s = self.spec()
         lv = _level(edge_index, node_attr.shape[0])
+        if node_attr.dtype == torch.float64:
+            return f64.node_update(self, node_attr, to_csc(edge_attr, lv), lv)
+        s = self.spec()
         s.pack.update(node_attr.dtype, node_attr.device)
         return NodeBlockFn.apply(node_attr, to_csc(edge_attr, lv), lv, s, torch.is_grad_enabled(), *s.node_params())
 
@@ -145,6 +152,8 @@ class MeshGraphNetLayer(nn.Module):
 
     def forward_level(self, node_attr, edge_attr, level):
         """Hot path: edge latents already in the level's receiver-grouped (CSC) order."""
+        if node_attr.dtype == torch.float64:
+            return f64.gmp_layer(self, node_attr, edge_attr, level)
         s = self.spec()
         s.pack.update(node_attr.dtype, node_attr.device)
         if _MEMLOG and not hasattr(self, '_edge_block_mem_logged'):

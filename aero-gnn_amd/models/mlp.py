@@ -49,6 +49,9 @@ class MLP(nn.Module):
         return self._spec
 
     def forward(self, x):
+        if x.dtype == torch.float64:  # train.py precision "double": agn_f64_* kernels (aerognn/f64.py)
+            from aerognn import f64
+            return f64.mlp_forward(self, x)
         if self.training and self.dropout.p > 0:
             raise NotImplementedError("aerognn fused MLP: dropout > 0 in training is not implemented")
         s = self.spec()
@@ -59,6 +62,9 @@ class MLP(nn.Module):
         """self.forward(x[rows]) with the row gather fused into the first layer's input loads (the
         kernel reads row rows[i] for output row i; no gathered copy): the edge encoder on the
         caller's edge features in a level's receiver-grouped order."""
+        if x.dtype == torch.float64:
+            from aerognn import f64
+            return f64.mlp_forward(self, x, rows)
         if self.training and self.dropout.p > 0:
             raise NotImplementedError("aerognn fused MLP: dropout > 0 in training is not implemented")
         s = self.spec()

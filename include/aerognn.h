@@ -36,7 +36,7 @@ extern "C" {
 #define AGN_MAX_LIN 8
 #define AGN_MAX_SEG 3
 
-enum { AGN_F32 = 0, AGN_BF16 = 1, AGN_F16 = 2 };
+enum { AGN_F32 = 0, AGN_BF16 = 1, AGN_F16 = 2, AGN_F64 = 3 };  /* F64: graph ops and the agn_f64_* entries */
 enum { AGN_SEG_PLAIN = 0, AGN_SEG_GATHER = 1, AGN_SEG_SUM = 2, AGN_SEG_MEAN = 3 };
 enum { AGN_E_ARG = -1, AGN_E_DTYPE = -2, AGN_E_HIDDEN = -3, AGN_E_SHAPE = -4 };
 
@@ -413,6 +413,51 @@ int agn_col_stats(int n, int k, const float* x, int ld, float* mean, float* std,
                   void* stream);
 int agn_collate(int B, int64_t ne, int64_t nn, const int64_t* edge_off, const int64_t* node_off, int64_t* edge_index,
                 int64_t* batch, void* stream);
+
+/* ---- float64 mode (train.py:20-40 precision "double" / "float64"): the MLP / GMP path in fp64
+ * on plain LDS-tiled FMA kernels (csrc/f64.hip); graph ops take dtype AGN_F64. */
+typedef struct {
+  const double* a;      /* operand rows: row r is a + (aidx ? aidx[r] : r) * lda, k columns */
+  const int32_t* aidx;  /* NULL, or gathered rows (x[src] / x[dst] of the concat edge MLP) */
+  int lda, k;
+  const double* w;      /* B(j, n) = transw ? w[n * ldw + j] : w[j * ldw + n] */
+  int ldw, transw;
+} agn_f64_seg;
+typedef struct {
+  int rows, n;          /* out [rows][n] */
+  int nseg;             /* <= 3 */
+  agn_f64_seg seg[3];
+  const double* bias;   /* [n] or NULL */
+  const double* add[2]; /* NULL or addends: add[q] + (add_idx[q] ? add_idx[q][r] : r) * add_ld[q] */
+  const int32_t* add_idx[2];
+  int add_ld[2];
+  const double* mask;   /* NULL, or out = 0 where mask <= 0 (ReLU backward on the saved activation) */
+  int mask_ld;
+  int relu;             /* out = max(out, 0) */
+  double* out;
+  int out_ld;
+} agn_f64_gemm_args;
+/* out = relu?(mask?(sum_seg A_seg B_seg + bias + add0 + add1)). Linear forward: transw = 1 (w = W
+ * + column offset, ldw = in_features); input gradient: transw = 0. mlp.py:40-51, mgnLayer.py:97-103 */
+int agn_f64_gemm(const agn_f64_gemm_args* a, void* stream);
+typedef struct {
+  int rows, m, k;
+  const double* g; int ldg;                  /* [rows][m] */
+  const double* x; int ldx;                  /* [rows][k], rows gathered by xidx if not NULL */
+  const int32_t* xidx;
+  double* dw; int ldw;                       /* [m][k] = g^T x (overwritten) */
+  double* db;                                /* [m] = colsum g, or NULL */
+} agn_f64_wgrad_args;
+size_t agn_f64_wgrad_scratch_bytes(const agn_f64_wgrad_args* a);
+int agn_f64_wgrad(const agn_f64_wgrad_args* a, void* scratch, void* stream);
+/* torch.nn.LayerNorm over the last n <= 1024 features (biased variance), y = ... + resid */
+int agn_f64_layernorm_fwd(int rows, int n, const double* x, int ldx, const double* gamma, const double* beta,
+                          const double* resid, int ldr, double* y, int ldy, double* mean, double* rstd, double eps,
+                          void* stream);
+size_t agn_f64_layernorm_bwd_scratch_bytes(int rows, int n);
+int agn_f64_layernorm_bwd(int rows, int n, const double* dy, int lddy, const double* x, int ldx, const double* mean,
+                          const double* rstd, const double* gamma, double* dx, int lddx, double* dgamma,
+                          double* dbeta, void* scratch, void* stream);
 
 #ifdef __cplusplus
 }

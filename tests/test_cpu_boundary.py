@@ -37,7 +37,11 @@ def test_struct_layouts_match_c(tmp_path):
               "agn_wgrad_desc": (L.WgradDesc, ["g", "x", "rows", "ldw", "dw_partial", "db", "nsplit", "xidx"]),
               "agn_wgrad_batch": (L.WgradBatch, ["n", "d"]),
               "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")]),
-              "agn_edge_bwd_args": (L.EdgeBwdArgs, [f for f, _ in L.EdgeBwdArgs._fields_])}
+              "agn_edge_bwd_args": (L.EdgeBwdArgs, [f for f, _ in L.EdgeBwdArgs._fields_]),
+              "agn_f64_seg": (L.F64Seg, [f for f, _ in L.F64Seg._fields_]),
+              "agn_f64_gemm_args": (L.F64GemmArgs, [f for f, _ in L.F64GemmArgs._fields_ if not f.startswith("_")]),
+              "agn_f64_wgrad_args": (L.F64WgradArgs, [f for f, _ in L.F64WgradArgs._fields_
+                                                      if not f.startswith("_")])}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "aerognn.h"', 'int main(void){']
     for st, (_, fs) in fields.items():
         lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
