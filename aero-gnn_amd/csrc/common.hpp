@@ -755,17 +755,6 @@ AGN_DEV f32x2 ln_out2(f32x2 v, float mean, float rstd, f32x2 g, f32x2 b) {
   return __builtin_elementwise_fma((v - f32x2{mean, mean}) * f32x2{rstd, rstd}, g, b);
 }
 
-// ---------------------------------------------------------------- L2 prefetch
-// Touch one 128-B line per lane so it is in L2 when a later load wants it: a 4-byte LDS-DMA load
-// (global_load_lds_dword) into a 256-B scratch area nobody reads. It needs no destination
-// register and nothing waits on it (the compiler's LDS alias tracking knows the scratch is
-// disjoint from every LDS read); it only adds one entry to vmcnt like any load.
-typedef __attribute__((address_space(1))) void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-AGN_DEV void prefetch_line(const void* p, void* lds_scratch) {
-  __builtin_amdgcn_global_load_lds((const gvoid_t*)p, (lvoid_t*)lds_scratch, 4, 0, 0);
-}
-
 // ---------------------------------------------------------------- wave reductions
 // The value a butterfly partner at distance M holds, with VALU cross-lane operations (no LDS
 // round trip, unlike __shfl_xor's ds_bpermute). M = 1, 2: DPP quad_perm (lane ^ M); M = 4: DPP

@@ -56,12 +56,7 @@ constexpr int OFF_PV = OFF_RING + NSLOT * SLOT_B;  // fp32 [4][H]: b1, b2, b3, L
 constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[4], consumed[4]
 constexpr int OFF_LNP = OFF_FLAG + 32;             // fp32 [CW][2][H]: LayerNorm partials per chain wave
 constexpr int OFF_IDS = OFF_LNP + CW * 2 * H * 4;   // int [CW][64]: next tile's src (lanes 0-31) / dst
-constexpr int OFF_PF = OFF_IDS + CW * 64 * 4;      // 256-B scratch of the L2 prefetches (never read)
-constexpr int LDS_B = OFF_PF + 256;
-#ifndef AGN_EB_PREFETCH
-#define AGN_EB_PREFETCH 0  // where the chain wave touches its next tile's rows: 0 off, 1 after the
-#endif                     // forward recompute, 2 after the LayerNorm backward, 3 after the L2 hand-off
-constexpr int EB_PF = AGN_EB_PREFETCH;
+constexpr int LDS_B = OFF_IDS + CW * 64 * 4;
 static_assert(LDS_B <= 160 * 1024, "LDS budget");
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -316,24 +311,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     return p[rr];
   };
   if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
-  // L2 prefetch of the next tile's rows (common.hpp prefetch_line, one line per lane and
-  // instruction): P_s[src] / P_d[dst] (two lines each), g2[dst], and the contiguous e and g tiles
-  auto prefetch_next = [&](int ntile, int nid, int lane) {
-    char* scr = lds + OFF_PF;
-    const int l = lane & 31;
-    const char* Pb = reinterpret_cast<const char*>(a.proj);
-    const char* prow = Pb + (size_t)nid * (4 * H) + (lane < 32 ? 0 : 2 * H);  // P_s | P_d segment
-    prefetch_line(prow, scr);
-    prefetch_line(prow + 128, scr);
-    const auto sw = __builtin_amdgcn_permlane32_swap((uint32_t)nid, (uint32_t)nid, false, false);
-    const int dst = lane < 32 ? (int)sw[1] : nid;  // row l's dst on both halves (common.hpp partner<32>)
-    prefetch_line(reinterpret_cast<const char*>(a.g2) + (size_t)dst * (2 * H) + (lane < 32 ? 0 : 128), scr);
-    const int erow = min(ntile * 32 + (lane >> 1), a.rows - 1);
-    const size_t eoff = (size_t)erow * (2 * H) + 128 * (lane & 1);
-    prefetch_line(reinterpret_cast<const char*>(a.e) + eoff, scr);
-    if (a.g) prefetch_line(reinterpret_cast<const char*>(a.g) + eoff, scr);
-    (void)l;
-  };
 
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
@@ -416,7 +393,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       gemm_rows(acc, a3, lds + 3 * IMG_B, fresh_lane(lane));
     }
     EB_STAMP(2);
-    if (EB_PF == 1 && more) prefetch_next(tile + rw.step * CW, nid, lane);
     // LayerNorm statistics (mlp_fwd_res_kernel's epilogue)
     float mean, rstd;
     {
@@ -533,7 +509,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       }
     }
     EB_STAMP(3);
-    if (EB_PF == 2 && more) prefetch_next(tile + rw.step * CW, nid, lane);
     // ---- chain rule; every layer's (G_L, a_L) goes to the dW waves
     BOp<bf16, NR> op;
     cbarrier();
@@ -567,7 +542,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
-    if (EB_PF == 3 && more) prefetch_next(tile + rw.step * CW, nid, lane);
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a2);  // G1

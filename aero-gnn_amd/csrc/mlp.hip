@@ -652,10 +652,6 @@ __device__ unsigned long long* agn_fwd_stamps;
   } while (0)
 #endif
 
-#ifndef AGN_FWD_PREFETCH
-#define AGN_FWD_PREFETCH 0  // 1: the resident edge forward touches its next tile's rows after the first GEMM
-#endif
-
 template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
@@ -666,7 +662,6 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
   __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e loads
   __shared__ int ids[RES_WPB][64];                     // per-wave next-tile src (lanes 0-31) / dst
-  __shared__ __attribute__((aligned(16))) int pfs[64];  // scratch of the L2 prefetches (never read)
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
   stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
@@ -741,16 +736,6 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     FWD_STAMP(2);
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
     FWD_STAMP(3);
-    if (AGN_FWD_PREFETCH && more) {
-      // L2 prefetch of the next tile's rows (common.hpp prefetch_line): P_s[src] / P_d[dst], two
-      // lines each, and the e rows
-      const char* prow = reinterpret_cast<const char*>(a.proj) + (size_t)nid * (2 * H * sizeof(T)) +
-                         (lane < 32 ? 0 : H * sizeof(T));
-      prefetch_line(prow, pfs);
-      prefetch_line(prow + 128, pfs);
-      const int erow = min((tile + tw.step) * 32 + (lane >> 1), a.rows - 1);
-      prefetch_line(reinterpret_cast<const char*>(sg.ptr) + ((size_t)erow * sg.ld + 64 * (lane & 1)) * sizeof(T), pfs);
-    }
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
