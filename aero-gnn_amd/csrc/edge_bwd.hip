@@ -571,6 +571,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
+#ifdef AGN_EB_NOSTORE  // diagnostic: the stores never issue (a runtime-false branch keeps the math)
+    if (a.rows == -12345)
+#endif
     op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     {
@@ -588,6 +591,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
           v[8 * i + e + 1] = o[1];
         }
       }
+#ifdef AGN_EB_NOSTORE
+      if (a.rows == -12345)
+#endif
       store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
     }
     EB_STAMP(11);

@@ -809,6 +809,9 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         }
       }
       if (i == 0 && more) wids[lane] = nid;  // (the slot's reads are done: LDS is in order per wave)
+#ifdef AGN_FWD_NOSTORE  // diagnostic: the stores never issue (a runtime-false branch keeps the math)
+      if (a.rows == -12345)
+#endif
       store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
     }
     FWD_STAMP(11);
