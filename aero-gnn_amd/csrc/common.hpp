@@ -286,6 +286,43 @@ AGN_DEV void store_row_w(T* rowp, const float (&v)[NR], int h, bool valid) {
   }
 }
 
+// A tile row's output held back as store-ready 16-B chunks, so that its stores issue after the
+// NEXT tile's loads: vmcnt counts loads and stores together in issue order, so a wait for a load
+// also waits for every store issued before it (measured: the edge kernels spent 10-18 % of
+// their time there). p == nullptr: nothing pending.
+template <int N>
+struct PendingRow {
+  u32x4 d[N];
+  bf16* p = nullptr;
+  bool valid = false;
+  // chunk i of a row in store8_w's layout (features 16 i + 8 h .. +7)
+  AGN_DEV void set(int i, const float (&v)[8]) {
+    uint32_t a0 = pack2(v[0], v[1]), a1 = pack2(v[2], v[3]), b0 = pack2(v[4], v[5]), b1 = pack2(v[6], v[7]);
+    swap_halves(a0, b0);
+    swap_halves(a1, b1);
+    d[i] = u32x4{a0, a1, b0, b1};
+  }
+  // the chunks of a packed operand (BOp<bf16>::store's layout)
+  template <class B>
+  AGN_DEV void set_op(const B& b) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const u32x4 x = __builtin_bit_cast(u32x4, b.u[i]);
+      uint32_t a0 = x[0], a1 = x[1], b0 = x[2], b1 = x[3];
+      swap_halves(a0, b0);
+      swap_halves(a1, b1);
+      d[i] = u32x4{a0, a1, b0, b1};
+    }
+  }
+  AGN_DEV void flush(int h) {
+    if (p && valid) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(p + 16 * i + 8 * h) = d[i];
+    }
+    p = nullptr;
+  }
+};
+
 // ---------------------------------------------------------------- AGN_TILED saves (aerognn.h)
 // 16-B unit index of (row, unit i of the lane's NR registers, half h); U = units per lane-row.
 template <typename T, int NR>
@@ -379,6 +416,13 @@ AGN_DEV void load8_tiled(float (&v)[8], const T* base, int i, int row, int h) {
 // Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
 // rows) above the MFMA chain, where they would sit live in registers across every layer.
 AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
+// a loaded value behind a compiler barrier: its first use (and the wait for the load) stays after
+// everything issued before this point (PendingRow flushes)
+AGN_DEV void hold_u4(uint4& x) {
+  u32x4 v = __builtin_bit_cast(u32x4, x);
+  asm volatile("" : "+v"(v));
+  x = __builtin_bit_cast(uint4, v);
+}
 // a value behind a compiler barrier: per-lane offsets derived from it are recomputed where used
 // instead of being hoisted out of a tile loop (where they would sit in registers and spill)
 AGN_DEV int opaque_v(int x) {

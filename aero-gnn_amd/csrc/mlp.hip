@@ -652,6 +652,10 @@ __device__ unsigned long long* agn_fwd_stamps;
   } while (0)
 #endif
 
+#ifndef AGN_FWD_DEFER
+#define AGN_FWD_DEFER 1  // resident edge forward: e' stores issue after the next tile's gathers
+#endif
+
 template <typename T, int NT>
 __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
@@ -686,6 +690,8 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #ifdef AGN_FWD_STAMPS
   int ntile = 0;
 #endif
+  // the previous tile's e' row, stored once this tile's gathers have issued (common.hpp PendingRow)
+  PendingRow<NR / 8> pend;
   for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
     // the lane id behind a barrier each tile: lane-derived offsets (row addresses, staging and
@@ -709,8 +715,30 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       const T* P = reinterpret_cast<const T*>(a.proj);
       // acc = P_s[src] + P_d[dst] on the matrix cores (exact fp32 add, common.hpp acc_add2_mfma)
       BOp<T, NR> xs, xd;
-      xs.load_w(P + (size_t)cs * (2 * H), h);
-      xd.load_w(P + (size_t)cd * (2 * H) + H, h);
+      {
+        // gathers issued, then the previous tile's stores, then the gathered data used: the wait
+        // for the gathers does not include the stores (PendingRow)
+        uint4 rs[NR / 8], rd[NR / 8];
+        const T* ps = P + (size_t)cs * (2 * H) + 8 * h;
+        const T* pd = P + (size_t)cd * (2 * H) + H + 8 * h;
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) {
+          rs[i] = *reinterpret_cast<const uint4*>(ps + 16 * i);
+          rd[i] = *reinterpret_cast<const uint4*>(pd + 16 * i);
+        }
+        if (AGN_FWD_DEFER) {
+          cbarrier();
+          pend.flush(h);
+          cbarrier();
+#pragma unroll
+          for (int i = 0; i < NR / 8; ++i) {
+            hold_u4(rs[i]);
+            hold_u4(rd[i]);
+          }
+        }
+        xs.set_w(rs);
+        xd.set_w(rd);
+      }
       bf16x8 f0, f1;
       ident_frags(f0, f1, lane);
       acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
@@ -722,11 +750,19 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       if (staged_in) {  // coalesced 1-KB loads through the wave's LDS staging rows
         tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
                                lane);
+        if (AGN_FWD_DEFER && !a.proj) {  // (nothing gathered: behind the e loads)
+          cbarrier();
+          pend.flush(h);
+        }
         uint4 mine[NR / 8];
         tile_load_finish<H / 8>(mine, eraw, stg[threadIdx.x >> 6], lane);
         b.set_w(mine);
       } else {
         b.load_w(reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
+        if (AGN_FWD_DEFER && !a.proj) {
+          cbarrier();
+          pend.flush(h);
+        }
       }
     }
     // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
@@ -809,16 +845,19 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
         }
       }
       if (i == 0 && more) wids[lane] = nid;  // (the slot's reads are done: LDS is in order per wave)
-#ifdef AGN_FWD_NOSTORE  // diagnostic: the stores never issue (a runtime-false branch keeps the math)
-      if (a.rows == -12345)
-#endif
-      store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
+      if (AGN_FWD_DEFER) pend.set(i, v);
+      else store8_w(op, i, h, v, valid);  // direct 16-B stores (the staged 1-KB store measured slower)
+    }
+    if (AGN_FWD_DEFER) {
+      pend.p = op;
+      pend.valid = valid;
     }
     FWD_STAMP(11);
 #ifdef AGN_FWD_STAMPS
     ++ntile;
 #endif
   }
+  if (AGN_FWD_DEFER) pend.flush(lane0 >> 5);
 }
 
 template <typename T, int NR>
