@@ -286,10 +286,10 @@ AGN_DEV void store_row_w(T* rowp, const float (&v)[NR], int h, bool valid) {
   }
 }
 
-// A tile row's output held back as store-ready 16-B chunks, so that its stores issue after the
-// NEXT tile's loads: vmcnt counts loads and stores together in issue order, so a wait for a load
-// also waits for every store issued before it (measured: the edge kernels spent 10-18 % of
-// their time there). p == nullptr: nothing pending.
+// A tile row's output held back as store-ready 16-B chunks, so that its stores issue once the
+// NEXT tile's loads have been waited for: vmcnt counts loads and stores together in issue order,
+// so a wait for a load also waits for every store issued before it (the edge kernels spent 10-18 %
+// of their time there). p == nullptr: nothing pending.
 template <int N>
 struct PendingRow {
   u32x4 d[N];
@@ -416,13 +416,7 @@ AGN_DEV void load8_tiled(float (&v)[8], const T* base, int i, int row, int h) {
 // Compiler-only barrier: keeps hipcc from hoisting later global loads (LN params, residual
 // rows) above the MFMA chain, where they would sit live in registers across every layer.
 AGN_DEV void cbarrier() { asm volatile("" ::: "memory"); }
-// a loaded value behind a compiler barrier: its first use (and the wait for the load) stays after
-// everything issued before this point (PendingRow flushes)
-AGN_DEV void hold_u4(uint4& x) {
-  u32x4 v = __builtin_bit_cast(u32x4, x);
-  asm volatile("" : "+v"(v));
-  x = __builtin_bit_cast(uint4, v);
-}
+
 // a value behind a compiler barrier: per-lane offsets derived from it are recomputed where used
 // instead of being hoisted out of a tile loop (where they would sit in registers and spill)
 AGN_DEV int opaque_v(int x) {

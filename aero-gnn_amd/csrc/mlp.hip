@@ -690,7 +690,7 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
 #ifdef AGN_FWD_STAMPS
   int ntile = 0;
 #endif
-  // the previous tile's e' row, stored once this tile's gathers have issued (common.hpp PendingRow)
+  // the previous tile's e' row, stored once this tile's loads have been consumed (PendingRow)
   PendingRow<NR / 8> pend;
   for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the (loop-invariant) LDS weight reads inside the loop: no LICM into VGPRs
@@ -726,16 +726,6 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
           rs[i] = *reinterpret_cast<const uint4*>(ps + 16 * i);
           rd[i] = *reinterpret_cast<const uint4*>(pd + 16 * i);
         }
-        if (AGN_FWD_DEFER) {
-          cbarrier();
-          pend.flush(h);
-          cbarrier();
-#pragma unroll
-          for (int i = 0; i < NR / 8; ++i) {
-            hold_u4(rs[i]);
-            hold_u4(rd[i]);
-          }
-        }
         xs.set_w(rs);
         xd.set_w(rd);
       }
@@ -750,19 +740,11 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
       if (staged_in) {  // coalesced 1-KB loads through the wave's LDS staging rows
         tile_load_issue<H / 8>(eraw, reinterpret_cast<const T*>(sg.ptr) + (size_t)tile * 32 * H, a.rows - tile * 32,
                                lane);
-        if (AGN_FWD_DEFER && !a.proj) {  // (nothing gathered: behind the e loads)
-          cbarrier();
-          pend.flush(h);
-        }
         uint4 mine[NR / 8];
         tile_load_finish<H / 8>(mine, eraw, stg[threadIdx.x >> 6], lane);
         b.set_w(mine);
       } else {
         b.load_w(reinterpret_cast<const T*>(sg.ptr) + (size_t)rr * sg.ld, h);
-        if (AGN_FWD_DEFER && !a.proj) {
-          cbarrier();
-          pend.flush(h);
-        }
       }
     }
     // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
@@ -772,6 +754,12 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp
     FWD_STAMP(2);
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
     FWD_STAMP(3);
+    if (AGN_FWD_DEFER) {
+      // the previous tile's e' stores issue here, after this tile's loads have been consumed:
+      // the next wait on a load is the next tile's, ~3/4 of a tile later, when they have completed
+      cbarrier();
+      pend.flush(h);
+    }
     for (int l = 1; l < a.nlin; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
