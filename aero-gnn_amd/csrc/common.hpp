@@ -314,10 +314,6 @@ struct PendingRow {
       d[i] = u32x4{a0, a1, b0, b1};
     }
   }
-  AGN_DEV void store_to(bf16* q, int h) const {
-#pragma unroll
-    for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(q + 16 * i + 8 * h) = d[i];
-  }
   AGN_DEV void flush(int h) {
     if (p && valid) {
 #pragma unroll

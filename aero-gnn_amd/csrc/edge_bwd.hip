@@ -48,14 +48,6 @@ constexpr int NSLOT = 3;
 #define AGN_EB_GROUP 2  // chain waves per hand-off group (item order, chain_wave)
 #endif
 constexpr int GROUP = AGN_EB_GROUP;
-#ifndef AGN_EB_DEFER
-#define AGN_EB_DEFER 1  // G0 / de stores of a tile issue after the next tile's first GEMM
-#endif
-constexpr bool EB_DEFER = AGN_EB_DEFER;
-#ifndef AGN_EB_DEFER_G0
-#define AGN_EB_DEFER_G0 1  // G0 too (with the g loads moved behind the flush: 0 spills; de alone: 2)
-#endif
-constexpr bool EB_DEFER_G0 = AGN_EB_DEFER && AGN_EB_DEFER_G0;
 constexpr int IMG_B = H * H * 2;       // one 128 x 128 bf16 image (32 KB)
 constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
 constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
@@ -320,10 +312,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   };
   if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
 
-  // the previous tile's G0 and de rows, stored once this tile's loads have been consumed
-  // (common.hpp PendingRow: a load wait also waits for every older store)
-  PendingRow<NR / 8> pg0, pde;
-  int prow_de = -1;  // the row pde holds (-1: none), instead of a live 64-bit pointer
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
     if (cw >= cmax) continue;
@@ -347,24 +335,22 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int sid = ids[c], did = ids[32 + c];
     const bool more = rd + rw.step < rw.end;
     const int nid = tile_id(more ? rd + rw.step : rd);  // stored to the slot before the tile's stores
-    // incoming gradient rows g and dAgg[dst], kept raw (64 registers) until the LayerNorm
-    // backward: loaded at the tile start, or (EB_DEFER) after the first GEMM, behind the previous
-    // tile's de stores, where they are off the register peak of the tile start
+    // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
+    // forward recompute
     uint4 graw[NR / 8], g2raw[NR / 8];
-    auto load_g = [&]() {
+    {
       const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H;
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) g2raw[i] = *reinterpret_cast<const uint4*>(g2p + 16 * i + 8 * h);
-      if (a.g) {
-        const bf16* gp = reinterpret_cast<const bf16*>(a.g) + (size_t)rr * H;
+    }
+    if (a.g) {
+      const bf16* gp = reinterpret_cast<const bf16*>(a.g) + (size_t)rr * H;
 #pragma unroll
-        for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
-      } else {
+      for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
+    } else {
 #pragma unroll
-        for (int i = 0; i < NR / 8; ++i) graw[i] = uint4{0u, 0u, 0u, 0u};
-      }
-    };
-    if (!EB_DEFER) load_g();
+      for (int i = 0; i < NR / 8; ++i) graw[i] = uint4{0u, 0u, 0u, 0u};
+    }
     // ---- forward recompute (mlp_fwd_res_kernel's operations, in its order)
     f32x16 acc[NT];
     BOp<bf16, NR> a1;  // the only activation kept from the forward pass
@@ -381,13 +367,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
       EB_STAMP(1);
       gemm_rows(acc, eop, lds + 0 * IMG_B, fresh_lane(lane));
-    }
-    if (EB_DEFER) {
-      cbarrier();
-      if (EB_DEFER_G0) pg0.flush(h);
-      if (prow_de >= 0) pde.store_to(reinterpret_cast<bf16*>(a.de) + (size_t)prow_de * H, h);
-      prow_de = -1;
-      load_g();
     }
     cbarrier();
     a1.template set_relu<NT>(acc);
@@ -592,13 +571,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
-    if (EB_DEFER_G0) {
-      pg0.set_op(op);
-      pg0.p = reinterpret_cast<bf16*>(a.g0) + (size_t)row * H;
-      pg0.valid = valid;
-    } else {
-      op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
-    }
+    op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     {
       float v[NR];
@@ -615,27 +588,12 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
           v[8 * i + e + 1] = o[1];
         }
       }
-      if (EB_DEFER) {
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) {
-          float o[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = v[8 * i + e];
-          pde.set(i, o);
-        }
-        prow_de = valid ? row : -1;
-      } else {
-        store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
-      }
+      store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.de) + (size_t)row * H, v, h, valid);
     }
     EB_STAMP(11);
 #ifdef AGN_EB_STAMPS
     ++ntile_done;
 #endif
-  }
-  if (EB_DEFER) {
-    if (EB_DEFER_G0) pg0.flush(lane0 >> 5);
-    if (prow_de >= 0) pde.store_to(reinterpret_cast<bf16*>(a.de) + (size_t)prow_de * H, lane0 >> 5);
   }
 }
 
