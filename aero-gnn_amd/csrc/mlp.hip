@@ -607,14 +607,6 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
 // one wave's gathers overlap the other waves' MFMA chains. One block per CU.
 constexpr int RES_WPB = 8;
 constexpr int RES_BLOCK = 64 * RES_WPB;
-constexpr int agn_res_wpb = RES_WPB;
-// waves per block of the resident edge forward: 8 (two per SIMD, 256 registers) or 12 (three per
-// SIMD, 168 registers: the residual operand is re-read from L2 and the stores are not deferred)
-#ifndef AGN_FWD_WPB
-#define AGN_FWD_WPB 8
-#endif
-constexpr int FWD_WPB = AGN_FWD_WPB;
-constexpr int FWD_BLOCK = 64 * FWD_WPB;
 constexpr int RES_MAXL = 4;
 // LDS-staged g loads / de stores in the resident backward: coalesced, but at 256 VGPRs the extra
 // live registers spill (measured: 2.55 -> 2.88 ms per launch with de staging), so both stay off
@@ -629,17 +621,17 @@ constexpr int res_layer_units() { return NT * (nrk(32 * NT) / BOp<T, 16>::RPU) *
 // share receivers and nearby senders: their P_s/P_d rows are re-read from the same L2.
 struct ResTiles {
   int first, end, step;
-  AGN_DEV ResTiles(int ntiles, int wid, int wpb = agn_res_wpb) {
+  AGN_DEV ResTiles(int ntiles, int wid) {
     if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
       const int g = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = gridDim.x >> 3;
       const int per = (ntiles + 7) / 8;
-      first = g * per + bi * wpb + wid;
+      first = g * per + bi * RES_WPB + wid;
       end = min(ntiles, (g + 1) * per);
-      step = nb * wpb;
+      step = nb * RES_WPB;
     } else {
-      first = blockIdx.x * wpb + wid;
+      first = blockIdx.x * RES_WPB + wid;
       end = ntiles;
-      step = gridDim.x * wpb;
+      step = gridDim.x * RES_WPB;
     }
   }
 };
@@ -661,28 +653,26 @@ __device__ unsigned long long* agn_fwd_stamps;
 #endif
 
 #ifndef AGN_FWD_DEFER
-#define AGN_FWD_DEFER (AGN_FWD_WPB == 8)  // resident edge forward: e' stores issue after the next tile's first GEMM
+#define AGN_FWD_DEFER 1  // resident edge forward: e' stores issue after the next tile's gathers
 #endif
 
 template <typename T, int NT>
-__global__ __launch_bounds__(FWD_BLOCK, FWD_WPB / 4) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
+__global__ __launch_bounds__(RES_BLOCK, 2) void mlp_fwd_res_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
   constexpr int NUH = nrk(H) / BOp<T, NR>::RPU;
   constexpr int LAYER = res_layer_units<T, NT>();
   __shared__ uint4 wres[RES_MAXL * LAYER];
   __shared__ __attribute__((aligned(16))) float pv[RES_MAXL + 2][H];  // biases, LN gamma, LN beta
-  // per-wave 8-row staging: coalesced e loads (not at 12 waves: no LDS left for it)
-  constexpr bool FWD_STAGE = FWD_WPB == 8;
-  __shared__ uint4 stg[FWD_STAGE ? FWD_WPB : 1][8][H / 8 + STG_PAD];
-  __shared__ int ids[FWD_WPB][64];                     // per-wave next-tile src (lanes 0-31) / dst
+  __shared__ uint4 stg[RES_WPB][8][H / 8 + STG_PAD];  // per-wave 8-row staging: coalesced e loads
+  __shared__ int ids[RES_WPB][64];                     // per-wave next-tile src (lanes 0-31) / dst
   for (int l = 0; l < a.nlin; ++l) stage_block(wres + l * LAYER, a.wpk[l], NUH, 0, NT, 0, NUH);
-  stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, FWD_BLOCK);
+  stage_params<H, RES_MAXL + 2>(pv, a.bias, a.nlin, a.ln_g, a.ln_b, RES_BLOCK);
   __syncthreads();
   const int lane0 = threadIdx.x & 63;
   const int ntiles = (a.rows + 31) / 32;
   const agn_seg& sg = a.seg[0];
-  const ResTiles tw(ntiles, threadIdx.x >> 6, FWD_WPB);
+  const ResTiles tw(ntiles, threadIdx.x >> 6);
   // The sender / receiver ids of the wave's next tile are loaded one tile ahead, so a tile's
   // projection-row gathers issue together with its e loads (one memory latency per tile, not two).
   // They reach the next tile through the wave's LDS slot, not a loop-carried register: a
@@ -716,7 +706,7 @@ __global__ __launch_bounds__(FWD_BLOCK, FWD_WPB / 4) void mlp_fwd_res_kernel(con
     BOp<T, NR> b;
     // the projection rows are gathered and summed first, then the e tile goes through the staging
     // rows (issuing the e loads ahead of the gathers measured slower: DESIGN.md §9, round 3)
-    const bool staged_in = FWD_STAGE && sg.ld == H;
+    const bool staged_in = sg.ld == H;
     uint4 eraw[NR / 8];
     const bool more = a.proj && tile + tw.step < tw.end;
     const int nid = tile_id(more ? tile + tw.step : tile);  // (unconditional: see tile_id)
@@ -759,7 +749,7 @@ __global__ __launch_bounds__(FWD_BLOCK, FWD_WPB / 4) void mlp_fwd_res_kernel(con
     }
     // the residual is the layer input itself (e' = e + .., mgnLayer.py:205): keep the packed
     // operand instead of re-reading the row in the epilogue
-    const bool res_in = FWD_WPB == 8 && a.resid == sg.ptr && a.out_ld == sg.ld;
+    const bool res_in = a.resid == sg.ptr && a.out_ld == sg.ld;
     const BOp<T, NR> e0 = b;
     FWD_STAMP(2);
     gemm<T, NT, NR, true>(acc, b, NUH, wres, NUH, NT, lane);
@@ -1199,9 +1189,9 @@ int num_cus() {
   }
   return g_cus;
 }
-int res_blocks(int rows, int wpb = RES_WPB) {
+int res_blocks(int rows) {
   const int tiles = (rows + 31) / 32;
-  const int need = (tiles + wpb - 1) / wpb;
+  const int need = (tiles + RES_WPB - 1) / RES_WPB;
   const int cap = num_cus();  // 128 KB of resident weights: one block per CU
   return need < cap ? (need > 0 ? need : 1) : cap;
 }
@@ -1309,8 +1299,8 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   }
   const bool vec = mode == M_VEC;
   if (res_fwd_ok(a, vec)) {
-    dim3 g(res_blocks(a->rows, FWD_WPB));
-    hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(FWD_BLOCK), 0, (hipStream_t)stream, *a);
+    dim3 g(res_blocks(a->rows));
+    hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
     return launch_status();
   }
   dim3 grid(agn_mlp_bwd_nwaves(a->rows));
