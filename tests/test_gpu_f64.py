@@ -128,3 +128,32 @@ def test_f64_model_train_step_vs_oracle(kind):
     print(f"f64 {kind} step: param-grad rel-L2 median {np.median(list(errs.values())):.3e}, "
           f"worst {errs[worst]:.3e} ({worst})")
     assert errs[worst] <= 1e-8, (worst, errs[worst])
+
+
+@pytest.mark.parametrize("method", ["mean", "max", "add"])
+def test_f64_poolmgn_vs_oracle(method):
+    """poolMGN (models/poolmgn.py, §8f row 4) in fp64 on a 3-mesh batch: global pooling (segment
+    sums / max in float64), broadcast, encoders, 4 layers, decoder; prediction and every parameter
+    gradient against the float64 oracle."""
+    from aerognn.meshgen import collate, ellipsoid
+    from models.poolmgn import poolMGN
+    from oracle import refcpu as R
+    b = collate([ellipsoid(30, 20, seed=s) for s in (0, 1)] + [ellipsoid(24, 12, seed=2)])
+    t = {k: torch.from_numpy(v) for k, v in b.items()}
+    kw = dict(processor_size=4, num_hidden_layers_node_processor=2, num_hidden_layers_edge_processor=2,
+              num_hidden_layers_node_encoder=2, num_hidden_layers_edge_encoder=2, num_hidden_layers_decoder=2,
+              aggregation="add", global_pool_method=method, num_hidden_layers_global_encoder=1, global_dim=128)
+    torch.manual_seed(0)
+    model = poolMGN(6, 4, 4, **kw).double()
+    x, ea, y = t["x"].double(), t["edge_attr"].double(), t["y"].double()
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in model.state_dict().items()}
+    ref = R.poolmgn_forward(p, x, ea, t["edge_index"], R.cfg_from_kwargs(**kw), batch=t["batch"])
+    torch.nn.functional.mse_loss(ref, y).backward()
+    model = model.to(DEV)
+    pred = model(x.to(DEV), ea.to(DEV), t["edge_index"].to(DEV), batch=t["batch"].to(DEV))
+    torch.nn.functional.mse_loss(pred, y.to(DEV)).backward()
+    _check(f"poolmgn {method} pred", pred, ref, 1e-9)
+    errs = {n: rel_l2(q.grad.detach().cpu(), p[n].grad) for n, q in model.named_parameters() if p[n].grad is not None}
+    worst = max(errs, key=errs.get)
+    print(f"f64 poolmgn {method}: param-grad rel-L2 worst {errs[worst]:.3e} ({worst})")
+    assert errs[worst] <= 1e-8, (worst, errs[worst])
