@@ -571,10 +571,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
-    // the re-read g / dAgg rows (issued before the L1 hand-off, long complete) are waited for
-    // BEFORE the G0 stores issue: vmcnt counts loads and stores in issue order, so the de
-    // epilogue's wait for them would otherwise also wait for these stores
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (expcnt, lgkmcnt untouched)
     op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     {
