@@ -1,4 +1,4 @@
-# Round-4 session t: the float64 tests (with poolMGN), then the C3 and C5 forward-only lines.
+# The float64 tests (with poolMGN), then the C3 and C5 forward-only lines.
 set -e
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,4 +1,4 @@
-# Round-4 session a: the GPU suite, the smoke check and the default bench line on this tree.
+# The GPU suite, the smoke check and the default bench line on this tree.
 # pytest exit 1 (test failures) continues to the smoke and the bench; any other non-zero status
 # (a crash, an abort, a time limit) ends the script.
 set -e
