@@ -105,8 +105,9 @@ def test_dp_grads_equal_union_batch_on_gpu(tmp_path, dt):
     if dt == "float64":
         assert errs.max() < 1e-10, errs.max()
     else:
-        # fp32 with different (valid) summation orders; ReLU kinks make a few parameters noisier
-        assert np.median(errs) < 1e-5 and errs.max() < 1e-3, (np.median(errs), errs.max())
+        # fp32 with different (valid) summation orders: measured median 6.9e-8, worst 1.3e-7
+        # (profiles/r4_gpu_tests.log); the gate leaves room for a ReLU-kink flip
+        assert np.median(errs) < 1e-6 and errs.max() < 1e-5, (np.median(errs), errs.max())
 
 
 def test_bench_two_ranks_json():
