@@ -62,6 +62,15 @@ __global__ __launch_bounds__(PJ_BLOCK, 2) void proj_kernel(int rows, const bf16*
   const Tiles tw(ntiles, wid);
   for (int tile = tw.first; tile < tw.end; tile += tw.step) {
     cbarrier();  // keep the LDS weight reads inside the loop
+    // one input segment (the forward's x): its tile is loaded once for both output groups, so
+    // group 1 does not reload it behind group 0's stores (a load wait also waits for every
+    // older store: DESIGN.md §9, round 4)
+    BOp<bf16, NR> b1;
+    if constexpr (NSEG == 1) {
+      uint4 mine[NR / 8];
+      tile_load_chunks<H / 8>(mine, x0 + (size_t)tile * 32 * x_ld, rows - tile * 32, stg[wid], lane, x_ld / 8);
+      b1.set_w(mine);
+    }
 #pragma unroll
     for (int grp = 0; grp < NGRP; ++grp) {
       f32x16 acc[NT];
@@ -76,11 +85,15 @@ __global__ __launch_bounds__(PJ_BLOCK, 2) void proj_kernel(int rows, const bf16*
       }
 #pragma unroll
       for (int s = 0; s < NSEG; ++s) {
-        uint4 mine[NR / 8];
-        tile_load_chunks<H / 8>(mine, (s == 0 ? x0 : x1) + (size_t)tile * 32 * x_ld, rows - tile * 32, stg[wid], lane,
-                                x_ld / 8);
         BOp<bf16, NR> b;
-        b.set_w(mine);
+        if constexpr (NSEG == 1) {
+          b = b1;
+        } else {
+          uint4 mine[NR / 8];
+          tile_load_chunks<H / 8>(mine, (s == 0 ? x0 : x1) + (size_t)tile * 32 * x_ld, rows - tile * 32, stg[wid],
+                                  lane, x_ld / 8);
+          b.set_w(mine);
+        }
         gemm<bf16, NT, NR, true>(acc, b, 8, w + ((size_t)grp * NT * KU + 8 * s) * 64, KU, NT, lane);
       }
       uint4 res[NR / 8];
