@@ -81,6 +81,12 @@ class EdgeBwdArgs(C.Structure):
                 ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp)]
 
 
+class EdgeFwdArgs(C.Structure):
+    _fields_ = [("rows", i32), ("nblk", i32), ("wpk", vp * 4), ("bias", vp * 4), ("ln_g", vp), ("ln_b", vp),
+                ("e", vp), ("proj", vp), ("src", vp), ("dst", vp), ("out", vp), ("act", vp * 3), ("hpre", vp),
+                ("stats", vp)]
+
+
 class PackDesc(C.Structure):
     _fields_ = [("src", vp), ("dst", vp), ("src_dtype", i32), ("dst_dtype", i32),
                 ("rows", i32), ("cols", i32), ("trans", i32), ("ld", i32),
@@ -117,6 +123,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
+            "agn_edge_forward", "agn_edge_backward",
             "agn_proj_forward", "agn_proj_backward")
 
 
@@ -214,6 +221,10 @@ def lib():
             "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),
             "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
+            "agn_edge_fwd_blocks": (i32, [i32]),
+            "agn_edge_forward": (i32, [C.POINTER(EdgeFwdArgs), vp]),
+            "agn_edge_backward_blocks": (i32, [i32]),
+            "agn_edge_backward": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_fault_status": (i32, [C.POINTER(i32), i32]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_proj_forward": (i32, [i32, vp, i32, vp, vp, vp, i32, vp]),

@@ -281,6 +281,7 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
 # AEROGNN_CHECK_FAULTS=1 (set by the test suite): read the device fault word after every
 # persistent hand-off launch (a device synchronisation each time; never on the timed path).
 CHECK_FAULTS = __import__("os").environ.get("AEROGNN_CHECK_FAULTS", "0") == "1"
+E16_SAVES = None  # parity tests: a list that the 16-row-tile edge forward appends its saves to
 STAMPS = None  # diagnostics: a uint64 device tensor of 2*8*8*16 entries (a -DAGN_EB_STAMPS library)
 
 
@@ -295,13 +296,43 @@ def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
             and nlin == 4 and has_ln and rows >= 64 * 1024)
 
 
-def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None):
-    """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm
-    partials [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce)."""
+def edge16_ok(dtype, hidden, nlin, has_ln):
+    """The 16-row-tile edge chain kernels (csrc/edge16*.hip: agn_edge_forward / agn_edge_backward)
+    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). AEROGNN_EDGE16=0 selects the
+    round-4 32-row kernels (agn_mlp_forward's resident kernel + agn_edge_bwd_fused) for A/B runs."""
+    import os
+    return (os.environ.get("AEROGNN_EDGE16", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
+            and nlin == 4 and has_ln)
+
+
+def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre=None, stats=None, tag=None,
+                 cost=None):
+    """agn_edge_forward: out = e + LN(chain(e, P_s[src] + P_d[dst])); acts / hpre / stats are optional
+    row-major saves (parity tests only)."""
+    lib = L.lib()
+    a = L.EdgeFwdArgs()
+    a.rows = int(rows)
+    a.nblk = int(lib.agn_edge_fwd_blocks(int(rows)))
+    for i in range(4):
+        a.wpk[i] = wpk[i]
+        a.bias[i] = bias[i]
+    a.ln_g, a.ln_b = ln
+    a.e, a.proj, a.src, a.dst, a.out = ptr(e), ptr(proj), ptr(src), ptr(dst), ptr(out)
+    for i in range(3):
+        a.act[i] = ptr(acts[i]) if acts is not None else None
+    a.hpre, a.stats = ptr(hpre), ptr(stats)
+    with timed(tag, cost):
+        check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
+
+
+def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False):
+    """agn_edge_backward (e16, the 16-row-tile kernel) or agn_edge_bwd_fused (round 4's 32-row
+    kernel); returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm partials
+    [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce)."""
     lib = L.lib()
     dev = e.device
     H = 128
-    nblk = int(lib.agn_edge_bwd_blocks(int(rows)))
+    nblk = int((lib.agn_edge_backward_blocks if e16 else lib.agn_edge_bwd_blocks)(int(rows)))
     dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
     dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
     lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
@@ -316,7 +347,10 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
     a.de, a.g0, a.dw_partial, a.db_partial, a.ln_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp), ptr(lnp)
     a.stamps = ptr(STAMPS)
     with timed(tag, cost):
-        check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
+        if e16:
+            check(lib.agn_edge_backward(C.byref(a), stream()), "edge_backward")
+        else:
+            check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
     if CHECK_FAULTS:  # tests / debug runs: a bounded ring wait that gave up is an error, not wrong dW
         f = L.fault_status(reset=True)
         if f:

@@ -21,7 +21,9 @@ import torch
 
 from . import _lib as L
 from ._lib import check, ptr
+from . import core as _core
 from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
+                   edge16_ok, edge_forward,
                    cost_edge_bwd_fused,
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
@@ -388,6 +390,9 @@ class GMPFn(torch.autograd.Function):
         x_out = torch.empty_like(x)
         # fused edge backward: the chain is recomputed there, the forward saves nothing for it
         fused = train and spec.trick and fused_edge_train_ok(E, dt, H, es.nlin, es.ln is not None)
+        # the 16-row-tile pair (agn_edge_forward / agn_edge_backward) whenever no split-path saves
+        # are needed: inference, and training with the fused backward
+        e16 = spec.trick and (fused or not train) and edge16_ok(dt, H, es.nlin, es.ln is not None)
         ea, ehp, est = _alloc_saves(es, E, dt, dev, train and not fused)
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         P = None
@@ -402,12 +407,26 @@ class GMPFn(torch.autograd.Function):
                             segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
                             wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
                             tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
-            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
-                        segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
-                        wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
-                        resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
-                        tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
-                                                                                            train and not fused)))
+            if e16:
+                # 16-row-tile kernel (csrc/edge16_fwd.hip); the fused backward recomputes it bitwise.
+                # core.E16_SAVES (parity tests only): also save a1..a3, h3 and the LN statistics
+                sv = None
+                if _core.E16_SAVES is not None:
+                    sv = ([torch.empty(E, H, dtype=dt, device=dev) for _ in range(3)],
+                          torch.empty(E, H, dtype=dt, device=dev), torch.empty(E, 2, dtype=torch.float32, device=dev))
+                    _core.E16_SAVES.append((E, e, P, level) + sv)
+                edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=level.src,
+                             dst=level.dst, out=e_out, acts=sv[0] if sv else None, hpre=sv[1] if sv else None,
+                             stats=sv[2] if sv else None,
+                             tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
+                                                                                                 False)))
+            else:
+                mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+                            segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
+                            wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
+                            resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
+                            tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
+                                                                                                train and not fused)))
         else:
             se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
             ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
@@ -434,7 +453,7 @@ class GMPFn(torch.autograd.Function):
                                                                  ns.nlin, train)))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
-        ctx.fused, ctx.proj = fused, (P if fused else None)
+        ctx.fused, ctx.proj, ctx.e16 = fused, (P if fused else None), e16
         ctx.save_for_backward(x, e)
         # an unused e' (the U-Net restores fine edges from the skip, bsms_mgn.py:203) arrives as
         # None instead of a materialised [E,H] zero tensor; the kernels read it as zero
@@ -473,7 +492,7 @@ class GMPFn(torch.autograd.Function):
             g0 = torch.empty(E, H, dtype=dt, device=dev)
             dW13, db13, part_e, nb_e = edge_bwd_fused(
                 rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=ctx.proj, src=lv.src, dst=lv.dst,
-                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd",
+                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd", e16=ctx.e16,
                 cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True), cost_edge_bwd_fused(E, N, H, sz)))
         else:
             nb_e = bwd_nblocks(E)

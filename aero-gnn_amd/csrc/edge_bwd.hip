@@ -788,6 +788,7 @@ int agn_edge_bwd_blocks(int rows) {
   return n < 8 ? 8 : n;
 }
 
+int agn_e16_fault_status(int* value, int reset);
 int agn_fault_status(int* value, int reset) {
   if (!value) return AGN_E_ARG;
   hipError_t e = hipDeviceSynchronize();
@@ -795,6 +796,12 @@ int agn_fault_status(int* value, int reset) {
   if (e == hipSuccess && reset) {
     const int zero = 0;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_agn_fault), &zero, sizeof(int));
+  }
+  int v16 = 0;
+  if (e == hipSuccess) {
+    const int r = agn_e16_fault_status(&v16, reset);
+    if (r != 0) return r;
+    *value |= v16;
   }
   return e == hipSuccess ? 0 : (int)e;
 }

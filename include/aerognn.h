@@ -379,6 +379,36 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
  * up and that launch's dW / db are wrong. Synchronises the device; reset != 0 clears the word. */
 #define AGN_FAULT_RING_TIMEOUT 1
 int agn_fault_status(int* value, int reset);
+/* ---- 16-row-tile sum-trick edge chain (bf16, H = 128; csrc/edge16*.hip) ----
+ * The same EdgeBlockSum chain (mgnLayer.py:72-105, residual :205) on v_mfma_f32_16x16x32_bf16
+ * 16-edge tiles: the forward keeps four waves per SIMD, and the fused backward two chain waves
+ * per SIMD beside the dW accumulators. The backward's forward recompute is bitwise
+ * agn_edge_forward's (shared k-order); the pair replaces agn_mlp_forward + agn_edge_bwd_fused
+ * for these chains.
+ *   agn_edge_forward : out = e + LN(chain(e, P_s[src] + P_d[dst])); act[0..2] (relu outputs
+ *                      a1..a3), hpre (pre-LN row) and stats (mean, rstd) are optional row-major
+ *                      saves for parity tests (NULL in production: the backward recomputes).
+ *   agn_edge_backward: agn_edge_bwd_args as agn_edge_bwd_fused, grid agn_edge_backward_blocks. */
+typedef struct {
+  int rows;                  /* edges (CSC order) */
+  int nblk;                  /* grid size: agn_edge_fwd_blocks(rows) */
+  const void* wpk[4];        /* packed A = W_l of W_e, Lin1, Lin2, Lin3 (agn_pack trans = 0, bf16) */
+  const float* bias[4];      /* fp32 biases; bias[1..3] of Lin1..Lin3 (bias[0] unused) */
+  const float* ln_g;         /* LayerNorm gamma, beta [128] */
+  const float* ln_b;
+  const void* e;             /* [rows][128] edge input = the residual */
+  const void* proj;          /* [N][256] P = [x W_s^T | x W_d^T + b] */
+  const int32_t* src;
+  const int32_t* dst;
+  void* out;                 /* [rows][128] e' */
+  void* act[3];              /* optional [rows][128] a1, a2, a3 */
+  void* hpre;                /* optional [rows][128] h3 (bf16) */
+  float* stats;              /* optional [rows][2] */
+} agn_edge_fwd_args;
+int agn_edge_fwd_blocks(int rows);
+int agn_edge_forward(const agn_edge_fwd_args* a, void* stream);
+int agn_edge_backward_blocks(int rows);
+int agn_edge_backward(const agn_edge_bwd_args* a, void* stream);
 /* dw[m][k] = sum_s dw_partial[s][m][k] (and db) for each desc: the fixed-order second stage
  * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);

@@ -1,0 +1,226 @@
+"""The 16-row-tile sum-trick edge chain (csrc/edge16_fwd.hip, csrc/edge16_bwd.hip) against float64.
+
+Reference chain: models/mgnLayer.py:72-105 (EdgeBlockSum) and the residual of :205, under autograd.
+Both kernels compute in bf16 with fp32 accumulation. Their tests here remove every source of
+difference except the kernels' own roundings:
+
+* forward, layer by layer: each layer's float64 product is formed from the KERNEL's previous
+  activation (a1..a3, saved row-major by agn_edge_forward's test outputs) and the bf16 weights the
+  kernel holds, then rounded to bf16 once; the kernel's activation must equal it except where the
+  fp32 accumulation lands on the other side of a bf16 rounding boundary (a few per million, one ulp);
+* backward, mask-matched: the float64 backward runs through the kernel's own ReLU masks and saved
+  bf16 activations (the forward's, which the fused backward recomputes bitwise), so no ReLU kink
+  flips between the two sides; what remains is the kernel's bf16 rounding of each G_L (~1e-3 per
+  rounding). Every output (de, G0, dW1..dW3, db1..db3, the LayerNorm partials) is gated at 3x its
+  measured rel-L2.
+"""
+import os
+
+import pytest
+import torch
+
+from golden_util import rel_l2
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("AEROGNN_MEMLOG", "0")
+DEV = "cuda"
+H = 128
+
+# measured on the MI355X (printed by the tests; profiles/r5_gpu_edge16_tests.log), gates 3x
+BWD_MEASURED = {"de": 2.0e-3, "g0": 3.0e-3, "dW1": 3.0e-3, "dW2": 3.0e-3, "dW3": 3.0e-3, "db1": 3.0e-3,
+                "db2": 3.0e-3, "db3": 3.0e-3, "dgamma": 1.0e-3, "dbeta": 1.0e-6}
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+class Chain:
+    """Random fp32 master parameters of one EdgeBlockSum chain (W_e, 3 Linears, LayerNorm), packed
+    as the model packs them (aerognn.functions.ChainSpec)."""
+
+    def __init__(self, seed):
+        from aerognn.core import Pack
+        from aerognn.functions import ChainSpec
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        s = H ** -0.5
+        self.we = (torch.randn(H, H, generator=g) * s).to(DEV)
+        self.w = [(torch.randn(H, H, generator=g) * s).to(DEV) for _ in range(3)]
+        self.b = [(torch.randn(H, generator=g) * 0.1).to(DEV) for _ in range(3)]
+        self.gamma = (1.0 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.beta = (0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.pack = Pack()
+        self.spec = ChainSpec([(self.we, None)] + list(zip(self.w, self.b)), (self.gamma, self.beta), H, self.pack, "e")
+        self.pack.update(torch.bfloat16, torch.device(DEV))
+
+
+def _level(N, E, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.to(torch.int32)
+    src = torch.randint(0, N, (E,), generator=g).to(torch.int32)
+    return src.to(DEV), dst.to(DEV)
+
+
+def _inputs(N, E, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed + 1)
+    e = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    P = torch.randn(N, 2 * H, generator=g).to(torch.bfloat16).to(DEV)
+    gi = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    g2 = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    return e, P, gi, g2
+
+
+def _forward(ch, e, P, src, dst):
+    from aerognn import core
+    E = e.shape[0]
+    out = torch.empty_like(e)
+    acts = [torch.empty_like(e) for _ in range(3)]
+    hpre = torch.empty_like(e)
+    stats = torch.empty(E, 2, dtype=torch.float32, device=DEV)
+    core.edge_forward(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P, src=src,
+                      dst=dst, out=out, acts=acts, hpre=hpre, stats=stats)
+    return out, acts, hpre, stats
+
+
+def _check_bf16_layer(name, got, ref64, relu):
+    """got (bf16) vs round(ref64) (with relu): equal except where the fp32 accumulation (absolute
+    error ~1e-6 on O(1) sums) lands on the other side of a bf16 rounding boundary: a few elements per
+    million, each within one ulp of the rounded value or within 1e-4 absolute (tiny values)."""
+    want = ref64.clamp_min(0.0) if relu else ref64
+    want = want.to(torch.bfloat16)
+    diff = got != want
+    frac = diff.double().mean().item()
+    worst = 0.0
+    if frac:
+        g, w = got[diff].double(), want[diff].double()
+        ulp = (w.abs() * 2.0 ** -7).clamp_min(2.0 ** -133)
+        worst = ((g - w).abs() / torch.maximum(ulp, torch.full_like(ulp, 1e-4))).max().item()
+    print(f"edge16 forward {name}: {frac:.2e} of the elements differ from the rounded float64 value "
+          f"(worst {worst:.2f} of max(1 ulp, 1e-4))")
+    assert frac <= 1e-4 and worst <= 1.0, (name, frac, worst)
+
+
+@pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (40000, 240000)])
+def test_edge16_forward_layers_vs_fp64(N, E):
+    ch = Chain(1)
+    src, dst = _level(N, E, 2)
+    e, P, _, _ = _inputs(N, E, 3)
+    out, acts, hpre, stats = _forward(ch, e, P, src, dst)
+    torch.cuda.synchronize()
+    we, w = _bf(ch.we), [_bf(x) for x in ch.w]
+    e64, P64 = e.double(), P.double()
+    h0 = e64 @ we.T + P64[src.long(), :H] + P64[dst.long(), H:]
+    _check_bf16_layer("a1", acts[0], h0, True)
+    prev = acts[0].double()
+    for l in range(2):
+        h = prev @ w[l].T + ch.b[l].double()
+        _check_bf16_layer(f"a{l + 2}", acts[l + 1], h, True)
+        prev = acts[l + 1].double()
+    h3 = prev @ w[2].T + ch.b[2].double()
+    _check_bf16_layer("h3", hpre, h3, False)
+    mean = h3.mean(1)
+    rstd = 1.0 / torch.sqrt(((h3 - mean[:, None]) ** 2).mean(1) + 1e-5)
+    rm = rel_l2(stats[:, 0].double(), mean)
+    rr = rel_l2(stats[:, 1].double(), rstd)
+    print(f"edge16 forward LN statistics: mean rel-L2 {rm:.2e}, rstd {rr:.2e}")
+    assert rm <= 1e-5 and rr <= 1e-5
+    y = _bf((h3 - mean[:, None]) * rstd[:, None] * ch.gamma.double() + ch.beta.double())
+    ref = _bf(y + e64)
+    r = rel_l2(out.double(), ref)
+    print(f"edge16 forward e': rel-L2 {r:.2e} against round(round(LN(h3)) + e)")
+    assert r <= 5e-3
+
+
+def _bwd_ref(ch, e, P, src, dst, gi, g2, acts, hpre, stats):
+    """float64 backward of the chain through the kernel's own masks and saved bf16 activations."""
+    a1, a2, a3 = (t.double() for t in acts)
+    we, w = _bf(ch.we), [_bf(x) for x in ch.w]
+    S = (gi.double() if gi is not None else 0.0) + g2.double()[dst.long()]
+    mean, rstd = stats[:, 0].double(), stats[:, 1].double()
+    xh = (hpre.double() - mean[:, None]) * rstd[:, None]
+    gg = S * ch.gamma.double()
+    c1 = gg.mean(1, keepdim=True)
+    c2 = (gg * xh).mean(1, keepdim=True)
+    G3 = (gg - c1 - xh * c2) * rstd[:, None]
+    out = {"dgamma": (S * xh).sum(0), "dbeta": S.sum(0), "dW3": G3.T @ a3, "db3": G3.sum(0)}
+    G2 = (G3 @ w[2]) * (a3 > 0)
+    out["dW2"], out["db2"] = G2.T @ a2, G2.sum(0)
+    G1 = (G2 @ w[1]) * (a2 > 0)
+    out["dW1"], out["db1"] = G1.T @ a1, G1.sum(0)
+    G0 = (G1 @ w[0]) * (a1 > 0)
+    out["g0"] = G0
+    out["de"] = G0 @ we + S
+    return out
+
+
+def _backward(ch, e, P, src, dst, gi, g2, e16=True):
+    from aerognn import core
+    from aerognn.core import colsum_rows
+    E = e.shape[0]
+    de, g0 = torch.empty_like(e), torch.empty_like(e)
+    dw, db, part, nb = core.edge_bwd_fused(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln_g=ch.spec.lnp()[0],
+                                           e=e, proj=P, src=src, dst=dst, g=gi, g2=g2, de=de, g0=g0, e16=e16)
+    ln = torch.empty(2 * H, dtype=torch.float32, device=DEV)
+    colsum_rows(part, nb, 2 * H, ln)
+    got = {"de": de, "g0": g0, "dgamma": ln[:H], "dbeta": ln[H:]}
+    for l in range(3):
+        got[f"dW{l + 1}"], got[f"db{l + 1}"] = dw[l], db[l]
+    return got
+
+
+@pytest.mark.parametrize("N,E,with_g", [(5000, 70001, True), (100000, 598400, True), (300, 17, True),
+                                        (20000, 100000, False)])
+def test_edge16_backward_mask_matched_fp64(N, E, with_g):
+    ch = Chain(5)
+    src, dst = _level(N, E, 6)
+    e, P, gi, g2 = _inputs(N, E, 7)
+    if not with_g:
+        gi = None
+    _, acts, hpre, stats = _forward(ch, e, P, src, dst)
+    got = _backward(ch, e, P, src, dst, gi, g2)
+    torch.cuda.synchronize()
+    ref = _bwd_ref(ch, e, P, src, dst, gi, g2, acts, hpre, stats)
+    fails = []
+    for k, v in ref.items():
+        r = rel_l2(got[k].double(), v)
+        gate = max(3.0 * BWD_MEASURED[k], 1e-6)
+        print(f"edge16 backward E={E} {k}: rel-L2 {r:.3e} against the mask-matched float64 backward (gate {gate:.1e})")
+        if not r <= gate:
+            fails.append((k, r))
+    assert not fails, fails
+
+
+def test_edge16_backward_deterministic_and_close_to_round4_kernel():
+    """Two launches give bitwise-equal outputs (fixed-order sums everywhere); the round-4 32-row
+    kernel (agn_edge_bwd_fused, different MFMA k-order) agrees to bf16 rounding."""
+    N, E = 20000, 130001
+    ch = Chain(9)
+    src, dst = _level(N, E, 10)
+    e, P, gi, g2 = _inputs(N, E, 11)
+    a = _backward(ch, e, P, src, dst, gi, g2)
+    b = _backward(ch, e, P, src, dst, gi, g2)
+    c = _backward(ch, e, P, src, dst, gi, g2, e16=False)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+        r = rel_l2(a[k].double(), c[k].double())
+        print(f"edge16 vs round-4 fused backward {k}: rel-L2 {r:.2e}")
+        assert r <= 5e-2, (k, r)
+
+
+def test_edge16_forward_close_to_round4_kernel():
+    from aerognn import core
+    from aerognn import _lib as L
+    N, E = 20000, 130001
+    ch = Chain(12)
+    src, dst = _level(N, E, 13)
+    e, P, _, _ = _inputs(N, E, 14)
+    out, _, _, _ = _forward(ch, e, P, src, dst)
+    old = torch.empty_like(e)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     ln=ch.spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=old)
+    torch.cuda.synchronize()
+    r = rel_l2(out.double(), old.double())
+    print(f"edge16 vs round-4 resident forward e': rel-L2 {r:.2e}")
+    assert r <= 5e-3
