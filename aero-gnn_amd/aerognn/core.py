@@ -142,6 +142,17 @@ class Pack:
 
     def _build(self, dtype, device):
         code = dt_code(dtype)
+        if code == L.F64:  # the float64 mode runs aerognn/f64.py on the unpacked parameters
+            raise NotImplementedError("aerognn Pack: packed MFMA operands are float32 / bfloat16 / float16")
+        for key, (M, K, parts) in self.mats.items():
+            for p in parts:
+                if p[0].dtype not in (torch.float32, torch.bfloat16, torch.float16):
+                    raise TypeError(f"aerognn Pack: {key} weights are {p[0].dtype}; model and activations must "
+                                    "share a float32 / bfloat16 / float16 dtype (or both be float64)")
+        for key, (n, parts) in self.vecs.items():
+            for p in parts:
+                if p[0].dtype not in (torch.float32, torch.bfloat16, torch.float16):
+                    raise TypeError(f"aerognn Pack: {key} parameters are {p[0].dtype}")
         offs = {}
         total = 0
         for key, (M, K, parts) in self.mats.items():
@@ -296,13 +307,17 @@ def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
             and nlin == 4 and has_ln and rows >= 64 * 1024)
 
 
-def edge16_ok(dtype, hidden, nlin, has_ln):
+def edge16_ok(dtype, hidden, nlin, has_ln, train):
     """The 16-row-tile edge chain kernels (csrc/edge16*.hip: agn_edge_forward / agn_edge_backward)
-    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). AEROGNN_EDGE16=0 selects the
-    round-4 32-row kernels (agn_mlp_forward's resident kernel + agn_edge_bwd_fused) for A/B runs."""
+    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). Inference uses the 16-row
+    forward (AEROGNN_EDGE16=0 turns it off). Training keeps the 32-row pair (agn_mlp_forward's
+    resident kernel + agn_edge_bwd_fused, bitwise-consistent recompute) unless AEROGNN_EDGE16_TRAIN=1:
+    the 16-row fused backward measured slower."""
     import os
-    return (os.environ.get("AEROGNN_EDGE16", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
-            and nlin == 4 and has_ln)
+    if not (os.environ.get("AEROGNN_EDGE16", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
+            and nlin == 4 and has_ln):
+        return False
+    return (not train) or os.environ.get("AEROGNN_EDGE16_TRAIN", "0") == "1"
 
 
 def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre=None, stats=None, tag=None,

@@ -221,7 +221,25 @@ class MLP64Fn(torch.autograd.Function):
         return (None, *dxs, *dadds, *dres, *pgrads)
 
 
+def _check_f64(chain, ts):
+    """Every operand of a float64 chain must be float64 on one device: the agn_f64_* kernels read
+    their buffers as doubles, so a float32 weight given a float64 input (a float32 model fed
+    torch.from_numpy data) would be read past its end. Raise as torch does for mm's operands."""
+    dev = None
+    for t in list(ts) + list(chain.params()):
+        if t is None:
+            continue
+        if t.dtype != F64:
+            raise TypeError(f"aerognn float64 path: expected all operands and parameters float64, got {t.dtype} "
+                            "(mat1 and mat2 must have the same dtype); call model.double() for float64 inputs")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f"aerognn float64 path: operands on {dev} and {t.device}")
+
+
 def run_chain(chain, xs, idxs=None, rows=None, adds=(), add_idx=(), resid=None):
+    _check_f64(chain, list(xs) + list(adds) + [resid])
     idxs = list(idxs) if idxs is not None else [None] * len(xs)
     if rows is None:
         rows = xs[0].shape[0] if idxs[0] is None else idxs[0].numel()

@@ -392,7 +392,7 @@ class GMPFn(torch.autograd.Function):
         fused = train and spec.trick and fused_edge_train_ok(E, dt, H, es.nlin, es.ln is not None)
         # the 16-row-tile pair (agn_edge_forward / agn_edge_backward) whenever no split-path saves
         # are needed: inference, and training with the fused backward
-        e16 = spec.trick and (fused or not train) and edge16_ok(dt, H, es.nlin, es.ln is not None)
+        e16 = spec.trick and (fused or not train) and edge16_ok(dt, H, es.nlin, es.ln is not None, train)
         ea, ehp, est = _alloc_saves(es, E, dt, dev, train and not fused)
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         P = None

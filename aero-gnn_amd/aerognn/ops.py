@@ -141,8 +141,10 @@ def _gather_bwd(ctx, g):
         return torch.ops.aerognn.scatter_sum(g, index, ctx.n, False), None, None
     # sum and divide in fp32 and round once, as the forward's in-kernel fp32 division does (a bf16
     # count would round group sizes above 256, a bf16 sum would round before the division)
-    d = torch.ops.aerognn.scatter_sum(g.float(), index, ctx.n, False)
-    cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).to(torch.float32)
+    # (16-bit types only: a float64 gradient stays float64, float32 is already fp32)
+    gs = g.float() if g.dtype in (torch.bfloat16, torch.float16) else g
+    d = torch.ops.aerognn.scatter_sum(gs, index, ctx.n, False)
+    cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).to(gs.dtype)
     return (d / cnt[:, None]).to(g.dtype), None, None
 
 

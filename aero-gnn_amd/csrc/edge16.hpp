@@ -31,6 +31,10 @@ namespace e16 {
 
 constexpr int H = 128;
 constexpr int IMG_B = H * H * 2;  // one 128 x 128 bf16 image (32 KB)
+#ifndef AGN_E16_PF
+#define AGN_E16_PF 2
+#endif
+constexpr int PF = AGN_E16_PF;    // weight fragments in flight per product (4 registers each)
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -91,16 +95,20 @@ AGN_DEV void gemm_fwd(f32x4 (&acc)[8], const Op& x, const char* lds, int img_off
   auto frag = [&](int idx) {
     const int t = idx >> 3, ob = idx & 7;
     const int ro = 256 * (32 * (ob >> 1) + 4 * (ob & 1));
+#ifdef AGN_E16_NOLDS  // diagnostic: no fragment reads (timing only; results wrong)
+    return __builtin_bit_cast(bf16x8, uint4{(uint32_t)(base + ro), (uint32_t)t, 0u, 0u});
+#endif
     const uint2 lo = *reinterpret_cast<const uint2*>(img + (base ^ (64 * t)) + ro);
     const uint2 hi = *reinterpret_cast<const uint2*>(img + (base ^ (64 * t) ^ 8) + ro);
     return frag2(lo, hi);
   };
-  bf16x8 f0 = frag(0), f1 = frag(1);
+  bf16x8 f[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) f[i] = frag(i);
 #pragma unroll
   for (int idx = 0; idx < 32; ++idx) {
-    const bf16x8 cur = f0;
-    f0 = f1;
-    if (idx + 2 < 32) f1 = frag(idx + 2);
+    const bf16x8 cur = f[idx % PF];
+    if (idx + PF < 32) f[idx % PF] = frag(idx + PF);
     acc[idx & 7] = mfma16(cur, x.u[idx >> 3], acc[idx & 7]);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -116,15 +124,19 @@ AGN_DEV void gemm_bwd(f32x4 (&acc)[8], const Op& gop, const char* lds, int img_o
   const int base = wimg(8 * g + q, p, 0);
   auto frag = [&](int idx) {
     const int ib = idx >> 2, t = idx & 3;
+#ifdef AGN_E16_NOLDS
+    return __builtin_bit_cast(bf16x8, uint4{(uint32_t)(base + ib), (uint32_t)t, 0u, 0u});
+#endif
     const char* pb = img + (base ^ (64 * (ib >> 1)) ^ (8 * (ib & 1)));
     return frag2(tr64(pb + 8192 * t), tr64(pb + 8192 * t + 1024));
   };
-  bf16x8 f0 = frag(0), f1 = frag(1);
+  bf16x8 f[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) f[i] = frag(i);
 #pragma unroll
   for (int idx = 0; idx < 32; ++idx) {
-    const bf16x8 cur = f0;
-    f0 = f1;
-    if (idx + 2 < 32) f1 = frag(idx + 2);
+    const bf16x8 cur = f[idx % PF];
+    if (idx + PF < 32) f[idx % PF] = frag(idx + PF);
     const int ib = idx >> 2, t = idx & 3;
     acc[ib] = t == 0 ? mfma16(cur, gop.u[0], f32x4{}) : mfma16(cur, gop.u[t], acc[ib]);
     __builtin_amdgcn_sched_barrier(0);

@@ -32,7 +32,11 @@ namespace {
 
 constexpr int CW = 8;                        // chain waves
 constexpr int DW = 8;                        // dW waves
+#ifdef AGN_E16_CHAINONLY  // diagnostic: the chain waves alone at 256 registers (no dW waves launched)
+constexpr int NTHR = 64 * CW;
+#else
 constexpr int NTHR = 64 * (CW + DW);
+#endif
 constexpr int ITEM_B = 2 * 16 * H * 2;       // G_L and a_L of 16 rows
 constexpr int OFF_RING = 4 * IMG_B;          // [3][ITEM_B], slot L-1
 constexpr int OFF_PV = OFF_RING + 3 * ITEM_B;  // fp32 [4][H]: b1, b2, b3, LN gamma

@@ -1119,6 +1119,11 @@ AGN_DEV void pack_one(const agn_pack_desc& d, int tid) {
 __global__ void pack_kernel(const agn_pack_desc* __restrict__ descs) {
   const agn_pack_desc d = descs[blockIdx.y];
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  // only float32 / bfloat16 / float16 operands are packed (the descriptors live in device memory, so
+  // the host wrapper (aerognn.core.Pack) rejects others; a stray one writes nothing here instead of
+  // reinterpreting its bits)
+  const auto ok = [](int t) { return t == AGN_F32 || t == AGN_BF16 || t == AGN_F16; };
+  if (!ok(d.src_dtype) || !ok(d.dst_dtype)) return;
   if (d.src_dtype == AGN_BF16) pack_one<bf16>(d, tid);
   else if (d.src_dtype == AGN_F16) pack_one<f16>(d, tid);
   else pack_one<float>(d, tid);

@@ -117,7 +117,7 @@ typedef struct {
 /* AGN_TILED layout of a [rows][H] activation saved for the backward (H = hidden, rows padded to
  * a multiple of 32): the 16-B register units of the 32-row wave that produced it, in register
  * order. Unit (row r, i, half h) lives at 16-B index ((r / 32) * U + i) * 64 + (r % 32) + 32 h,
- * U = H * elem_size / 16; for bf16 it holds features 16i+4h+{0..3} and 16i+8+4h+{0..3}, for fp32
+ * U = (H / 2) * elem_size / 16 (units per lane half-row); for bf16 it holds features 16i+4h+{0..3} and 16i+8+4h+{0..3}, for fp32
  * features 8i+4h+{0..3}. One wave store/load instruction moves 1 KB contiguous. Only libaerognn
  * kernels read it (the MLP backward and agn_wgrad). */
 
@@ -192,7 +192,9 @@ enum { AGN_OPT_RESIDENT = 0 };
 int agn_set_option(int key, int value);
 /* bytes of a packed A operand with `m` rows and `k` reduction columns */
 size_t agn_packed_bytes(int m, int k, int dtype);
-/* max_threads >= max over descs of packed 16-B units (or vector length) */
+/* max_threads >= max over descs of packed 16-B units (or vector length). src_dtype / dst_dtype must be
+ * AGN_F32 / AGN_BF16 / AGN_F16; a descriptor with another dtype (it lives in device memory, so it
+ * cannot be checked here without a copy) writes nothing. */
 int agn_pack(const agn_pack_desc* descs_device, int n, int max_threads, void* stream);
 
 int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream);

@@ -38,6 +38,7 @@ def test_struct_layouts_match_c(tmp_path):
               "agn_wgrad_batch": (L.WgradBatch, ["n", "d"]),
               "agn_wec_args": (L.WecArgs, [f for f, _ in L.WecArgs._fields_ if not f.startswith("_")]),
               "agn_edge_bwd_args": (L.EdgeBwdArgs, [f for f, _ in L.EdgeBwdArgs._fields_]),
+              "agn_edge_fwd_args": (L.EdgeFwdArgs, [f for f, _ in L.EdgeFwdArgs._fields_]),
               "agn_f64_seg": (L.F64Seg, [f for f, _ in L.F64Seg._fields_]),
               "agn_f64_gemm_args": (L.F64GemmArgs, [f for f, _ in L.F64GemmArgs._fields_ if not f.startswith("_")]),
               "agn_f64_wgrad_args": (L.F64WgradArgs, [f for f, _ in L.F64WgradArgs._fields_
@@ -140,3 +141,17 @@ def test_poolmgn_state_dict_and_errors():
     model.load_state_dict(params(d))
     with pytest.raises(ValueError):
         poolMGN(6, 4, 4, global_pool_method="median")
+
+
+def test_pack_rejects_float64_and_mixed_dtypes():
+    """a float64 model (or a float64 weight in a 16/32-bit pack) raises on the host
+    instead of being packed as float bits (agn_pack reads descriptors from device memory)."""
+    import torch
+    from aerognn.core import Pack
+    w = torch.randn(128, 128, dtype=torch.float64)
+    p = Pack()
+    p.matrix("W", 128, 128, [(w, 0, 0, False)])
+    with pytest.raises(NotImplementedError):
+        p.update(torch.float64, torch.device("cpu"))
+    with pytest.raises(TypeError):
+        p.update(torch.float32, torch.device("cpu"))

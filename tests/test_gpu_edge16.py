@@ -1,4 +1,6 @@
-"""The 16-row-tile sum-trick edge chain (csrc/edge16_fwd.hip, csrc/edge16_bwd.hip) against float64.
+"""The fused sum-trick edge chain backward kernels against a mask-matched float64 backward:
+agn_edge_bwd_fused (the 32-row training default, csrc/edge_bwd.hip) and the 16-row-tile pair
+(csrc/edge16_fwd.hip, csrc/edge16_bwd.hip: the inference forward; AEROGNN_EDGE16_TRAIN=1 trains on it).
 
 Reference chain: models/mgnLayer.py:72-105 (EdgeBlockSum) and the residual of :205, under autograd.
 Both kernels compute in bf16 with fp32 accumulation. Their tests here remove every source of
@@ -26,9 +28,12 @@ os.environ.setdefault("AEROGNN_MEMLOG", "0")
 DEV = "cuda"
 H = 128
 
-# measured on the MI355X (printed by the tests; profiles/r5_gpu_edge16_tests.log), gates 3x
-BWD_MEASURED = {"de": 2.0e-3, "g0": 3.0e-3, "dW1": 3.0e-3, "dW2": 3.0e-3, "dW3": 3.0e-3, "db1": 3.0e-3,
-                "db2": 3.0e-3, "db3": 3.0e-3, "dgamma": 1.0e-3, "dbeta": 1.0e-6}
+# worst rel-L2 over the parametrised cases, measured on the MI355X for both kernels (identical to 3
+# digits: the rounding points are the same; profiles/r5_gpu_edge16_tests.log); each gate is 3x. The
+# float64 side does not round G_L to bf16, the kernels do (~1e-3 per rounding, accumulating down the
+# chain); the LayerNorm partials are fp32 sums of fp32 products (~1e-7).
+BWD_MEASURED = {"de": 2.41e-3, "g0": 3.36e-3, "dW1": 2.75e-3, "dW2": 2.32e-3, "dW3": 1.58e-3, "db1": 2.71e-3,
+                "db2": 2.34e-3, "db3": 1.59e-3, "dgamma": 1.6e-7, "dbeta": 1.5e-7}
 
 
 def _bf(t):
@@ -168,23 +173,55 @@ def _backward(ch, e, P, src, dst, gi, g2, e16=True):
     return got
 
 
+def _decode_tiled(t, rows):
+    """AGN_TILED [rows_pad, 128] bf16 -> row-major [rows, 128] (aerognn.h: unit (i, h) of row c holds
+    features 16i+4h+{0..3}, 16i+8+4h+{0..3})."""
+    u = t.view(torch.int16).reshape(-1, 8, 2, 32, 8)  # [tile][i][h][c][8]
+    out = torch.empty(u.shape[0], 32, H, dtype=torch.int16, device=t.device)
+    for i in range(8):
+        for hh in range(2):
+            v = u[:, i, hh]
+            out[:, :, 16 * i + 4 * hh:16 * i + 4 * hh + 4] = v[:, :, :4]
+            out[:, :, 16 * i + 8 + 4 * hh:16 * i + 8 + 4 * hh + 4] = v[:, :, 4:]
+    return out.reshape(-1, H)[:rows].view(torch.bfloat16)
+
+
+def _forward_32(ch, e, P, src, dst):
+    """The 32-row resident forward (agn_mlp_forward) with the split path's saves (AGN_TILED): the
+    activations the 32-row fused backward recomputes bitwise."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves
+    E = e.shape[0]
+    out = torch.empty_like(e)
+    acts, hpre, stats = _alloc_saves(ch.spec, E, torch.bfloat16, torch.device(DEV), True)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     ln=ch.spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=out, acts=acts, hpre=hpre, stats=stats)
+    return out, [_decode_tiled(a, E) for a in acts], _decode_tiled(hpre, E), stats
+
+
+@pytest.mark.parametrize("kernel", ["edge16", "fused32"])
 @pytest.mark.parametrize("N,E,with_g", [(5000, 70001, True), (100000, 598400, True), (300, 17, True),
                                         (20000, 100000, False)])
-def test_edge16_backward_mask_matched_fp64(N, E, with_g):
+def test_edge_backward_mask_matched_fp64(kernel, N, E, with_g):
+    """each fused backward against the float64 backward run through the kernel's
+    own ReLU masks and bf16 saves (the forward whose recompute the kernel reproduces bitwise)."""
     ch = Chain(5)
     src, dst = _level(N, E, 6)
     e, P, gi, g2 = _inputs(N, E, 7)
     if not with_g:
         gi = None
-    _, acts, hpre, stats = _forward(ch, e, P, src, dst)
-    got = _backward(ch, e, P, src, dst, gi, g2)
+    e16 = kernel == "edge16"
+    _, acts, hpre, stats = (_forward if e16 else _forward_32)(ch, e, P, src, dst)
+    got = _backward(ch, e, P, src, dst, gi, g2, e16=e16)
     torch.cuda.synchronize()
     ref = _bwd_ref(ch, e, P, src, dst, gi, g2, acts, hpre, stats)
     fails = []
     for k, v in ref.items():
         r = rel_l2(got[k].double(), v)
-        gate = max(3.0 * BWD_MEASURED[k], 1e-6)
-        print(f"edge16 backward E={E} {k}: rel-L2 {r:.3e} against the mask-matched float64 backward (gate {gate:.1e})")
+        gate = 3.0 * BWD_MEASURED[k]
+        print(f"{kernel} backward E={E} {k}: rel-L2 {r:.3e} against the mask-matched float64 backward (gate {gate:.1e})")
         if not r <= gate:
             fails.append((k, r))
     assert not fails, fails

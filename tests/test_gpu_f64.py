@@ -157,3 +157,13 @@ def test_f64_poolmgn_vs_oracle(method):
     worst = max(errs, key=errs.get)
     print(f"f64 poolmgn {method}: param-grad rel-L2 worst {errs[worst]:.3e} ({worst})")
     assert errs[worst] <= 1e-8, (worst, errs[worst])
+
+
+def test_f64_input_to_float32_model_raises():
+    """a float32 MLP given a float64 input raises TypeError (as torch's mm does)
+    instead of the agn_f64_* kernels reading the float32 weights as doubles."""
+    from models.mlp import MLP
+    m = MLP(16, 32, 8, 1, use_layer_norm=True).to(DEV)
+    x = torch.randn(100, 16, dtype=torch.float64, device=DEV)
+    with pytest.raises(TypeError):
+        m(x)

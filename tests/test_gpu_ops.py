@@ -48,6 +48,24 @@ def test_gather_rows_and_backward():
     assert torch.equal(s.grad.cpu(), torch.zeros_like(src).index_add_(0, idx, w))
 
 
+def test_gather_rows_mean_backward_float64_stays_float64():
+    """the mean-gather backward sums and divides a float64 gradient in float64 (only 16-bit
+    types are upcast to fp32)."""
+    import aerognn.ops  # noqa: F401
+    n, k = 5000, 8
+    g = torch.Generator().manual_seed(5)
+    idx = torch.sort(torch.randint(0, 40, (n,), generator=g)).values
+    rowptr = torch.searchsorted(idx, torch.arange(41))
+    src = torch.randn(40, k, dtype=torch.float64, generator=g)
+    w = torch.randn(n, k, dtype=torch.float64, generator=g)
+    s = src.to(DEV).requires_grad_(True)
+    (torch.ops.aerognn.gather_rows(s, idx.to(DEV), rowptr.to(DEV)) * w.to(DEV)).sum().backward()
+    cnt = (rowptr[1:] - rowptr[:-1]).clamp(min=1).double()
+    ref = torch.zeros(40, k, dtype=torch.float64).index_add_(0, idx, w) / cnt[:, None]
+    assert s.grad.dtype == torch.float64
+    assert torch.allclose(s.grad.cpu(), ref, rtol=1e-13, atol=1e-13)
+
+
 def test_gather_rows_mean_backward_bf16_large_groups():
     """gather_rows with a group-size divisor (the broadcast side of a mean pool): its backward sums
     and divides in fp32 and rounds once, so a 100,000-row group's gradient is the fp32 value rounded

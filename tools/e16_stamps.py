@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--nu", type=int, default=1000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--stamps", action="store_true", help="AEROGNN_LIB is a stamps build: print phase clocks")
+    ap.add_argument("--save", default=None, help="save the raw stamps [2][16][8][16] (.npy)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -65,11 +66,14 @@ def main():
         for _ in range(2):
             f()
         torch.cuda.synchronize()
-        t = time.perf_counter()
-        for _ in range(args.reps):
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.reps)]
+        for a, b in ev:
+            a.record()
             f()
+            b.record()
         torch.cuda.synchronize()
-        print(f"E = {E}: edge16 {name} {1e3 * (time.perf_counter() - t) / args.reps:.3f} ms per launch")
+        ms = sorted(a.elapsed_time(b) for a, b in ev)
+        print(f"E = {E}: edge16 {name} {ms[len(ms) // 2]:.3f} ms per launch (median of {args.reps}, HIP events)")
     if not args.stamps:
         return
     core.STAMPS = torch.zeros(2 * 16 * 8 * 16, dtype=torch.int64, device=dev)
@@ -77,6 +81,8 @@ def main():
     torch.cuda.synchronize()
     st = core.STAMPS.cpu().numpy().astype(np.int64).reshape(2, 16, 8, 16)
     core.STAMPS = None
+    if args.save:
+        np.save(args.save, st)
     ch = st[:, :8]  # chain waves
     d = np.diff(ch, axis=-1)  # [2, 8, 8, 15] phase durations
     tile = ch[..., 15] - ch[..., 0]
