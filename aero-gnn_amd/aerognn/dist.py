@@ -110,6 +110,9 @@ class GradAllReduce:
         self._pending = None
         self._hooks = []
         self.launched_in_hooks = 0  # buckets the last armed backward launched from its hooks
+        # optional: a list that __call__ appends (start, end) HIP-event pairs to, bracketing the
+        # all-reduce work left after the backward (the exposed part: remaining launches, waits, unpack)
+        self.exposed_events = None
         if active():
             where = {}
             for bi, b in enumerate(self.buckets):
@@ -163,6 +166,10 @@ class GradAllReduce:
     def __call__(self):
         if not active():
             return
+        ev = None
+        if self.exposed_events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for bi in range(len(self.buckets)):  # the rest, in index order
             if bi not in self._works:
                 self._launch(bi)
@@ -179,3 +186,6 @@ class GradAllReduce:
                 p.grad.copy_(flat[o:o + n].view_as(p.grad))
                 o += n
         self._works = {}
+        if ev is not None:
+            ev[1].record()
+            self.exposed_events.append(ev)

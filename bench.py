@@ -51,8 +51,9 @@ CONFIGS = {
     "c5": (2500, 2000, 6, torch.bfloat16),
     "small": (200, 125, 4, torch.bfloat16),
     "c4": (400, 250, 4, torch.bfloat16),
+    "c4small": (40, 25, 4, torch.bfloat16),  # the C4 leg's shape at test size (tests/test_gpu_dist.py)
 }
-BATCHED = {"c4": (64, 8)}  # config: (global batch of meshes, meshes per micro-batch)
+BATCHED = {"c4": (64, 8), "c4small": (4, 2)}  # config: (global batch of meshes, meshes per micro-batch)
 MODEL_NAME = "BiStridedMeshGraphNet(H=128, n_hid=2, processor_size=15, stride=2, concat_trick)"
 
 
@@ -379,6 +380,8 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=1, help="extra instrumented steps for the kernel table")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="skip the secondary C4 strong-scaling measurement")
+    ap.add_argument("--strong-config", default=None, choices=sorted(BATCHED),
+                    help="run the strong-scaling leg on this batched config (default: c4 after a c3 train run)")
     ap.add_argument("--cpu-plan", action="store_true", help="run BASELINE.md §3's full CPU plan and exit")
     ap.add_argument("--traffic", default=latest_profile("pmc_traffic.json"),
                     help="tools/pmc_traffic.py output: PMC-derived HBM bytes per launch of the hot kernels "
@@ -478,7 +481,9 @@ def main():
                         fwd(b)
         return step
 
-    def timed_run(step, steps, warmup):
+    def timed_run(step, steps, warmup, per_rank=None):
+        """Wall time of `steps` steps bracketed by barrier + synchronize, the MAX over ranks; with
+        per_rank a dict, also each rank's own time (min / max over ranks)."""
         for _ in range(warmup):
             step()
         torch.cuda.synchronize()
@@ -492,12 +497,22 @@ def main():
         if ws > 1:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
+        own = elapsed
         if ws > 1:
             e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             if D._host_staged():
                 e = e.cpu()
             torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
             elapsed = float(e.item())
+        if per_rank is not None:
+            lo = own
+            if ws > 1:
+                m = torch.tensor([own], dtype=torch.float64, device=dev)
+                if D._host_staged():
+                    m = m.cpu()
+                torch.distributed.all_reduce(m, op=torch.distributed.ReduceOp.MIN)
+                lo = float(m.item())
+            per_rank.update(rank_ms_min=1e3 * lo / steps, rank_ms_max=1e3 * elapsed / steps)
         return elapsed
 
     model, batches, eu_step, Es, workload, scaling, extra = setup(args.config)
@@ -610,13 +625,23 @@ def main():
         out["collective"] = {"backend": torch.distributed.get_backend(), "world_size": ws,
                              "buckets": len(allreduce_ref[0].buckets) if allreduce_ref else None,
                              "launched_in_hooks": allreduce_ref[0].launched_in_hooks if allreduce_ref else None}
-    if args.model == "bsms_mgn" and args.config == "c3" and args.mode == "train" and not args.no_c4:
+    strong = args.strong_config or ("c4" if args.config == "c3" else None)
+    if args.model == "bsms_mgn" and strong and args.mode == "train" and not args.no_c4:
         del model, batches, step
         torch.cuda.empty_cache()
-        m4, b4, eu4, _, wl4, _, ex4 = setup("c4")
+        m4, b4, eu4, _, wl4, _, ex4 = setup(strong)
         st4 = make_step(m4, b4, ex4)
         k4 = min(args.steps, 5)
-        el4 = timed_run(st4, k4, 1)
+        ar4 = allreduce_ref[0]
+        ar4.exposed_events = [] if D.active() else None
+        pr4 = {}
+        el4 = timed_run(st4, k4, 1, per_rank=pr4)
+        exposed = None
+        if ar4.exposed_events:  # the timed steps' brackets (the warm-up's first one dropped)
+            torch.cuda.synchronize()
+            evs = ar4.exposed_events[-k4:]
+            exposed = sum(a.elapsed_time(b) for a, b in evs) / len(evs)
+        ar4.exposed_events = None
         eu4_all = eu4 * ws
         if ws > 1:
             t4 = torch.tensor([float(eu4)], dtype=torch.float64, device=dev)
@@ -627,13 +652,25 @@ def main():
         out["c4_strong"] = {"value": round(eu4_all * k4 / el4 / 1e6, 2), "unit": "M edge-updates/s",
                             "ms_per_step": round(1e3 * el4 / k4, 3), "steps": k4, "warmup": 1, "scaling": "strong",
                             "workload": wl4, "edge_updates_per_step_per_gpu": eu4,
+                            "rank_ms_min": round(pr4["rank_ms_min"], 3), "rank_ms_max": round(pr4["rank_ms_max"], 3),
+                            "allreduce_exposed_ms": round(exposed, 3) if exposed is not None else None,
+                            "allreduce_note": "rank 0's all-reduce work left after the backward (remaining bucket "
+                                              "launches, waits, unpack), HIP events on the compute stream; "
+                                              "null at world size 1 (no collective)",
                             "note": "BASELINE.json configs[3] / north_star's 1->8 scaling case (fixed global batch)"}
+    # the persistent hand-off kernels' device fault word (agn_fault_status): a bounded LDS-ring wait
+    # that gave up anywhere in this run means wrong dW; the line carries it and the run fails
+    from aerognn import _lib as L
+    fault = L.fault_status(reset=False)
+    out["fault_word"] = fault
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and args.model == "bsms_mgn":
         out["cpu_baseline"] = cpu_baseline(S)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if D.active():
         torch.distributed.destroy_process_group()
+    if fault:
+        raise SystemExit(f"bench: device fault word {fault:#x} (an LDS-ring wait of the fused edge backward gave up)")
 
 
 if __name__ == "__main__":

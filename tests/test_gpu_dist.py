@@ -125,7 +125,8 @@ def test_bench_self_launch_two_ranks_json():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", AEROGNN_DIST_BACKEND="gloo", AEROGNN_MEMLOG="0")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--config", "small", "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline"], env=env, cwd=ROOT, capture_output=True, text=True, timeout=500)
+                        "--no-cpu-baseline", "--strong-config", "c4small"], env=env, cwd=ROOT, capture_output=True,
+                       text=True, timeout=500)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]  # rank 0 prints the only line
@@ -134,6 +135,12 @@ def test_bench_self_launch_two_ranks_json():
     assert d["n_gpus"] == 2 and d["value"] > 0 and d["config"]["parallelism"] == "dp2"
     assert d["collective"]["world_size"] == 2 and d["collective"]["backend"] == "gloo"
     assert d["config"]["edge_updates_per_step_all_ranks"] > d["config"]["edge_updates_per_step_per_gpu"]
+    # the strong-scaling leg reports per-rank times and the exposed all-reduce
+    c4 = d["c4_strong"]
+    print(c4)
+    assert 0 < c4["rank_ms_min"] <= c4["rank_ms_max"] and c4["rank_ms_max"] == pytest.approx(c4["ms_per_step"], rel=1e-3)
+    assert c4["allreduce_exposed_ms"] is not None and c4["allreduce_exposed_ms"] >= 0.0
+    assert d["fault_word"] == 0
 
 
 def test_bench_rejects_world_size_mismatch():
