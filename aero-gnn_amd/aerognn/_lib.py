@@ -78,7 +78,8 @@ class WecArgs(C.Structure):
 class EdgeBwdArgs(C.Structure):
     _fields_ = [("rows", i32), ("nblk", i32), ("wpk", vp * 4), ("bias", vp * 4), ("ln_g", vp), ("e", vp),
                 ("proj", vp), ("src", vp), ("dst", vp), ("g", vp), ("g2", vp), ("de", vp), ("g0", vp),
-                ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp)]
+                ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp), ("dpd", vp),
+                ("rowptr", vp), ("nodes", i32)]
 
 
 class EdgeFwdArgs(C.Structure):

@@ -340,10 +340,13 @@ def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre
         check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
 
 
-def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False):
-    """agn_edge_backward (e16, the 16-row-tile kernel) or agn_edge_bwd_fused (round 4's 32-row
-    kernel); returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm partials
-    [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce)."""
+def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False,
+                   dpd=None, rowptr=None):
+    """agn_edge_backward (e16, the 16-row-tile kernel) or agn_edge_bwd_fused (the 32-row kernel);
+    returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm partials [nblk, 256]
+    fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce). With dpd ([N, 128], the
+    32-row kernel only) and rowptr (the receivers' CSC offsets) it also writes dP_d, bitwise
+    segment_sum(N, 128, rowptr, None, g0)."""
     lib = L.lib()
     dev = e.device
     H = 128
@@ -361,6 +364,10 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
     a.g, a.g2 = ptr(g), ptr(g2)
     a.de, a.g0, a.dw_partial, a.db_partial, a.ln_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp), ptr(lnp)
     a.stamps = ptr(STAMPS)
+    if dpd is not None:
+        if e16 or rowptr is None:
+            raise ValueError("edge_bwd_fused: dpd needs the 32-row kernel and rowptr")
+        a.dpd, a.rowptr, a.nodes = ptr(dpd), ptr(rowptr), int(dpd.shape[0])
     with timed(tag, cost):
         if e16:
             check(lib.agn_edge_backward(C.byref(a), stream()), "edge_backward")

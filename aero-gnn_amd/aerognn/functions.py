@@ -490,9 +490,11 @@ class GMPFn(torch.autograd.Function):
         if fused:
             # one launch: forward recompute, LayerNorm backward, chain rule, dW1..dW3 / db1..db3
             g0 = torch.empty(E, H, dtype=dt, device=dev)
+            # the 32-row kernel also forms dP_d (the receiver sums of G0) on its dW waves
+            dPd = None if ctx.e16 else torch.empty(N, H, dtype=dt, device=dev)
             dW13, db13, part_e, nb_e = edge_bwd_fused(
                 rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=ctx.proj, src=lv.src, dst=lv.dst,
-                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd", e16=ctx.e16,
+                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd", e16=ctx.e16, dpd=dPd, rowptr=lv.rowptr,
                 cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True), cost_edge_bwd_fused(E, N, H, sz)))
         else:
             nb_e = bwd_nblocks(E)
@@ -517,7 +519,8 @@ class GMPFn(torch.autograd.Function):
         if spec.trick:
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
             dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
-            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
+            if not fused or dPd is None:
+                dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
             if proj_kernel_ok(dx, H):
                 s_el = dx.element_size()
                 proj_backward(N, dPs, dPd, spec.pack["projT"], dx, tag="proj_bwd",

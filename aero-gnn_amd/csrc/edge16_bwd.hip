@@ -553,7 +553,7 @@ int agn_e16_fault_status(int* value, int reset) {
 
 int agn_edge_backward(const agn_edge_bwd_args* a, void* stream) {
   if (!a || a->rows < 1 || a->nblk < 1 || !a->e || !a->proj || !a->src || !a->dst || !a->g2 || !a->ln_g ||
-      !a->de || !a->g0 || !a->dw_partial || !a->db_partial || !a->ln_partial)
+      !a->de || !a->g0 || !a->dw_partial || !a->db_partial || !a->ln_partial || a->dpd)
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;

@@ -597,6 +597,191 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   }
 }
 
+// ------------------------------------------------------------------------------ dP_d
+// P_d = x W_d^T + b enters h0 of every edge of its receiver (mgnLayer.py:72-105), so dP_d[n] is
+// the sum of G0 over n's edges: agn_segment_sum's fp32 sum in edge order from zero, rounded once.
+// The dW waves form it on chip: dW wave d recomputes features 32d..32d+31 of G0 for each tile
+// from the tile's L1 hand-off (G1, a1) and walks the tile's 32 rows in order, carrying the open
+// receiver's sum from tile to tile of a round (the L1 pairs arrive in tile order) and restarting
+// it at every change of receiver. The walk stores the running sum of EVERY row to dP_d[dst[row]]:
+// one wave's stores to one address land in program order, so a receiver's last store is its
+// whole sum, and the walk needs no branch per row. Receivers whose edges span a 128-row round
+// boundary get partial sums from two rounds; dpd_cross_kernel, launched after the fused kernel,
+// overwrites them (and writes the empty receivers' zeros).
+constexpr int ROUND_ROWS = CW * 32;
+
+struct DpdWalk {
+  int cur;    // receiver of the open run (-1 at a round's start: the round's first row opens one)
+  float sum;  // its fp32 sum (lanes 0-31: feature 32d + lane)
+  int dvn;    // receivers of the next L1 pair's tile (lanes 0-31), loaded a pair ahead
+#ifdef AGN_EB_STAMPS
+  unsigned long long t_mm = 0, t_walk = 0;  // cycles in the G0 recompute (to the release) / the walk
+#endif
+};
+
+// receivers of a tile's rows (lane c & 31: row 32 tile + c, clamped to the last row)
+AGN_DEV int dpd_ids(const agn_edge_bwd_args& a, int tile, int lane) {
+  return a.dst[min(tile * 32 + (lane & 31), a.rows - 1)];
+}
+
+// one row of the walk: restart the sum at a new receiver, add the row, store the running sum.
+// A raw buffer store over the 64-byte slice dP_d[n][32d..32d+31]: lanes 32-63 address past its
+// end and are dropped by the range check, so the store needs no exec-mask branch (voff).
+AGN_DEV void dpd_row(const agn_edge_bwd_args& a, DpdWalk& st, int n, float v, int d, int voff) {
+  st.sum = (n != st.cur ? 0.f : st.sum) + v;
+  st.cur = n;
+  bf16* rowp = reinterpret_cast<bf16*>(a.dpd) + ((size_t)n * H + 32 * d);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rowp, 0, 64, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, (bf16)st.sum), rs, voff, 0, 0);
+}
+
+// dP_d of a tile's L1 pair (ring slots k0, k1), then release() the slots. The ring reads stream
+// under the MFMAs (one fragment in flight: the dW wave's 192 accumulators leave no room to hold
+// the pair's 40 registers of G1 / a1 across a release) and the slots are released after the
+// last MFMA, before the row walk.
+template <typename Release>
+AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k1, int tile, int next_tile, int d,
+                      int lane, DpdWalk& st, Release release) {
+#ifdef AGN_EB_STAMPS
+  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+  lane = fresh_lane(lane);  // lane-derived offsets are formed here, not hoisted out of the dW loop
+  const int c = lane & 31, hh = lane >> 5;
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  // [a1 > 0] at D's places, as 16 bits: transposed reads of the items' a1 images. Register 4m + j
+  // of lane (c, hh) is row 8m + 4hh + j, feature 32d + c; lane 4j + p of each 16-lane group
+  // supplies row 8m + 4hh + j at image positions 32d + 16(g&1) + 4 sw(p) (sw swaps p's bits: phi),
+  // so lane t of the group receives feature 32d + 16(g&1) + t. Relu outputs are +0 or positive
+  // int16 patterns (relu_select_pk's mask rule).
+  int keep = 0;
+  {
+    const int xm = 2 * (g & 1) + (p & 1);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const char* sa = lds + OFF_RING + ((m >> 1) ? k1 : k0) * SLOT_B + HALF_B;
+      const int off = 2048 * (m & 1) + 512 * d + 64 * (4 * hh + q) + 16 * (xm ^ (2 * (m & 1) + hh)) + 8 * (p >> 1);
+      const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sa + off));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) keep |= (v[j] > 0 ? 1 : 0) << (4 * m + j);
+    }
+  }
+  // D[row c'][f] = sum_k G1[c'][k] W1[k][32d + f]: the chain's last gemm_cols step (ot = d) with the
+  // operands swapped: A = the chain's own G1 operand read back from the ring (lane (c, hh) of k-step
+  // u: chunk 2u + hh of row c), B = gemm_cols' W1^T fragment. Same products, same k order, so D is
+  // the transpose of the chain's accumulator, bitwise.
+  f32x16 D;
+  {
+    const char* sg = lds + OFF_RING + ((c >> 4) ? k1 : k0) * SLOT_B;
+    const int r = c & 15, x = (r >> 2) & 3;
+    const int base = 2048 * (r >> 3) + 64 * (r & 7);
+    const int oe = base + 16 * (hh ^ x), oo = base + 16 * ((2 + hh) ^ x);
+    const int xx = 2 * (g & 1) + (p & 1);
+    const char* img = lds + 1 * IMG_B + 512 * d;
+    const char* r1 = img + 64 * (4 * hh + q) + 16 * (xx ^ hh) + 8 * (p >> 1);
+    const char* r2 = img + 2048 + 64 * (4 * hh + q) + 16 * (xx ^ (hh + 2)) + 8 * (p >> 1);
+    auto ga = [&](int u) { return *reinterpret_cast<const uint4*>(sg + (u & 1 ? oo : oe) + 512 * (u >> 1)); };
+    auto wb = [&](int u) { return tr_pair(r1 + 4096 * u, r2 + 4096 * u); };
+    uint4 a0 = ga(0);
+    bf16x8 b0 = wb(0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint4 ca = a0;
+      const bf16x8 cb = b0;
+      if (u + 1 < 8) {
+        a0 = ga(u + 1);
+        b0 = wb(u + 1);
+      }
+      D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ca), cb, u == 0 ? f32x16{} : D, 0, 0, 0);
+      sched_fence();
+    }
+  }
+  lgkm_drain();
+  release();
+#ifdef AGN_EB_STAMPS
+  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+  st.t_mm += c1 - c0;
+#endif
+  // G0 = round(D) where a1 > 0
+  float gv[16];
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const uint32_t pk = pack2(D[k], D[k + 1]);
+    gv[k] = (keep >> k) & 1 ? lo_bf16(pk) : 0.f;
+    gv[k + 1] = (keep >> (k + 1)) & 1 ? hi_bf16(pk) : 0.f;
+  }
+  // the receivers, waited for once (an opaque copy: no per-row waits behind the walk's stores)
+  int dvw = st.dvn;
+  opaque(dvw);
+  if (next_tile >= 0) st.dvn = dpd_ids(a, next_tile, lane);
+  const int nval = min(32, a.rows - tile * 32);
+  const int voff = hh ? 64 : 2 * c;  // dpd_row's store offset (lanes 32-63: dropped)
+  // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
+  // lanes 0-31 take over by v_permlane32_swap, four registers at a time. Full tiles walk
+  // straight-line code; only the last tile of the edge list checks its row count.
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = gv[4 * m + j];
+      v[4 + j] = __uint_as_float(
+          __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[4 * m + j]), __float_as_uint(gv[4 * m + j]), false, false)[1]);
+    }
+    if (nval == 32) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpd_row(a, st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], d, voff);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (8 * m + j < nval) dpd_row(a, st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], d, voff);
+    }
+    sched_fence();
+  }
+#ifdef AGN_EB_STAMPS
+  st.t_walk += __builtin_amdgcn_s_memtime() - c1;
+#endif
+}
+
+// receivers the in-kernel walk does not finish (edges spanning a round boundary: the walk left
+// partial sums there) and empty ones, after the fused kernel: segment_sum_kernel's thread layout
+// and summation order (16 threads per receiver, 8 features each)
+__global__ __launch_bounds__(256) void dpd_cross_kernel(int nodes, const int32_t* __restrict__ ptr,
+                                                        const bf16* __restrict__ g0, bf16* __restrict__ dpd) {
+  const int sub = threadIdx.x & 15;
+  const int n = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (n >= nodes) return;
+  const int beg = ptr[n], end = ptr[n + 1];
+  if (end > beg && beg / ROUND_ROWS == (end - 1) / ROUND_ROWS) return;  // summed in the fused kernel
+  const int f0 = 8 * sub;
+  auto ld8 = [&](float (&o)[8], int row) {
+    const u32x4 x = *reinterpret_cast<const u32x4*>(g0 + (size_t)row * H + f0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[2 * i] = lo_bf16(x[i]);
+      o[2 * i + 1] = hi_bf16(x[i]);
+    }
+  };
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int j = beg;
+  for (; j + 1 < end; j += 2) {
+    float x[8], y[8];
+    ld8(x, j);
+    ld8(y, j + 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
+  }
+  if (j < end) {
+    float x[8];
+    ld8(x, j);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] += x[i];
+  }
+  u32x4 w;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = pack2(s[2 * i], s[2 * i + 1]);
+  *reinterpret_cast<u32x4*>(dpd + (size_t)n * H + f0) = w;
+}
+
 // ------------------------------------------------------------------------------ dW wave
 AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
 #ifdef AGN_EB_NORING
@@ -632,8 +817,11 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   unsigned long long waited = 0;
   const unsigned long long tstart = __builtin_amdgcn_s_memtime();
 #endif
+  DpdWalk dw_run{-1, 0.f, 0};
+  if (a.dpd && rw.first < rw.end) dw_run.dvn = dpd_ids(a, rw.first * CW, lane);
   for (int rd = rw.first; rd < rw.end; rd += rw.step) {
     const int cmax = min(CW, ntiles - rd * CW);
+    dw_run.cur = -1;  // a round's first row opens a run (one that began earlier is dpd_cross_kernel's)
     for (int grp = 0; grp < CW / GROUP; ++grp) {  // the chain waves' item order (chain_wave): group, layer, wave
     const int gsz = GROUP == 2 ? (grp == 0 ? min(2, cmax) : max(0, cmax - 2)) : (grp < cmax ? 1 : 0);
 #pragma unroll
@@ -668,10 +856,15 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
           xf[q2][1] = tr_pair(sb + HALF_B + 512 * (ib + 1) + t1, sb + HALF_B + 512 * (ib + 1) + t2);
         }
         lgkm_drain();
-        if (lane == 0) {
-          __hip_atomic_fetch_add(&consumed[k0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          __hip_atomic_fetch_add(&consumed[k1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        auto release = [&]() {
+          if (lane == 0) {
+            __hip_atomic_fetch_add(&consumed[k0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&consumed[k1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        };
+        // an L1 pair with dP_d is released after its dP_d reads (dpd_pair)
+        const bool dp = li == 2 && a.dpd;
+        if (!dp) release();
 #ifdef AGN_EB_STAMPS
         if (ist && lane == 0) ist[2] = ist[5] = __builtin_amdgcn_s_memtime();
 #endif
@@ -692,6 +885,12 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
             }
           }
         }
+        if (dp) {
+          sched_fence();  // the dW MFMAs have taken gf / xf before these reads claim registers
+          const int t = grp * GROUP + cc;  // the L1 pairs come in tile order
+          const int nxt = t + 1 < cmax ? rd * CW + t + 1 : (rd + rw.step < rw.end ? (rd + rw.step) * CW : -1);
+          dpd_pair(a, lds, k0, k1, rd * CW + t, nxt, d, lane, dw_run, release);
+        }
       }
     }
     }
@@ -702,6 +901,8 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
     sp[0] = waited;
     sp[1] = __builtin_amdgcn_s_memtime() - tstart;
     sp[2] = (unsigned long long)n;
+    sp[3] = dw_run.t_mm;
+    sp[4] = dw_run.t_walk;
   }
 #endif
   // partial slabs (true feature order): dW_L of workgroup b at dw_partial[(L-1) nblk + b][o][i]
@@ -812,7 +1013,16 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;
+  if (a->dpd && (!a->rowptr || a->nodes < 1 || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
+                 (reinterpret_cast<uintptr_t>(a->g0) & 15)))
+    return AGN_E_ARG;
   hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
+  if (a->dpd) {
+    const int st = launch_status();
+    if (st) return st;
+    hipLaunchKernelGGL(dpd_cross_kernel, dim3((a->nodes + 15) / 16), dim3(256), 0, (hipStream_t)stream, a->nodes,
+                       a->rowptr, (const bf16*)a->g0, (bf16*)a->dpd);
+  }
   return launch_status();
 }
 

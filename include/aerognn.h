@@ -373,6 +373,14 @@ typedef struct {
   float* db_partial;         /* [3][nblk][128] */
   float* ln_partial;         /* [nblk][2][128]: sum g * xhat, sum g (LayerNorm weight / bias grads) */
   unsigned long long* stamps; /* diagnostics only (a -DAGN_EB_STAMPS build): NULL, or [2][8][8][16] */
+  /* optional (agn_edge_bwd_fused only; agn_edge_backward rejects a non-NULL dpd): dP_d, the
+   * receiver segment sums of G0, bitwise agn_segment_sum(nodes, 128, BF16, rowptr, NULL, g0, ..).
+   * The dW waves recompute their 32 features of G0 from each tile's L1 hand-off and sum the
+   * receiver runs that lie inside one 128-row round; a second launch on the same stream sums the
+   * receivers whose edges span a round boundary, and zeroes the empty ones. */
+  void* dpd;                 /* [nodes][128] out, or NULL */
+  const int32_t* rowptr;     /* [nodes + 1] receiver offsets of dst (dst sorted: CSC order) */
+  int nodes;
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);

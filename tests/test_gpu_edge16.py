@@ -227,6 +227,53 @@ def test_edge_backward_mask_matched_fp64(kernel, N, E, with_g):
     assert not fails, fails
 
 
+def _dst_cases():
+    g = torch.Generator(device="cpu").manual_seed(21)
+    yield "random deg 14", 5000, torch.sort(torch.randint(0, 5000, (70001,), generator=g)).values
+    yield "random deg 6, empty receivers", 100000, torch.sort(torch.randint(0, 100000, (598400,), generator=g)).values
+    yield "tiny", 300, torch.sort(torch.randint(0, 300, (17,), generator=g)).values
+    yield "deg 500: every run spans rounds", 200, torch.sort(torch.randint(0, 200, (100000,), generator=g)).values
+    yield "one receiver", 3, torch.ones(5000, dtype=torch.int64)
+    # runs ending exactly on round boundaries (128 rows) and single-edge receivers between them
+    deg = torch.tensor([128, 1, 127, 128, 256, 1, 1, 126, 3, 125, 129], dtype=torch.int64)
+    yield "round-aligned runs", 12, torch.repeat_interleave(torch.arange(11) + 1, deg)
+
+
+@pytest.mark.parametrize("case", list(range(6)))
+def test_fused_backward_dpd_bitwise_segment_sum(case):
+    """the 32-row fused backward's dP_d (receiver sums of G0 formed on its dW
+    waves + dpd_cross_kernel) equals agn_segment_sum over the G0 it writes, bit for bit; the launch's
+    other outputs are those of a launch without dP_d."""
+    from aerognn import core
+    name, N, dst = list(_dst_cases())[case]
+    E = dst.numel()
+    ch = Chain(15)
+    g = torch.Generator(device="cpu").manual_seed(16 + case)
+    src = torch.randint(0, N, (E,), generator=g).to(torch.int32).to(DEV)
+    dst = dst.to(torch.int32).to(DEV)
+    rowptr = torch.zeros(N + 1, dtype=torch.int32, device=DEV)
+    rowptr[1:] = torch.cumsum(torch.bincount(dst.long(), minlength=N), 0).to(torch.int32)
+    e, P, gi, g2 = _inputs(N, E, 17 + case)
+
+    def run(with_dpd):
+        de, g0 = torch.empty_like(e), torch.empty_like(e)
+        dpd = torch.full((N, H), float("nan"), dtype=torch.bfloat16, device=DEV) if with_dpd else None
+        dw, db, part, _ = core.edge_bwd_fused(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                                              ln_g=ch.spec.lnp()[0], e=e, proj=P, src=src, dst=dst, g=gi, g2=g2,
+                                              de=de, g0=g0, dpd=dpd, rowptr=rowptr)
+        return de, g0, dw, db, part, dpd
+
+    de, g0, dw, db, part, dpd = run(True)
+    de2, g02, dw2, db2, part2, _ = run(False)
+    want = core.segment_sum(N, H, rowptr, None, g0, torch.empty(N, H, dtype=torch.bfloat16, device=DEV))
+    torch.cuda.synchronize()
+    for a, b in ((de, de2), (g0, g02), (dw, dw2), (db, db2), (part, part2)):
+        assert torch.equal(a, b)
+    nd = (dpd.view(torch.int16) != want.view(torch.int16)).sum().item()
+    print(f"fused backward dP_d [{name}] N={N} E={E}: {nd} of {N * H} elements differ from agn_segment_sum")
+    assert nd == 0
+
+
 def test_edge16_backward_deterministic_and_close_to_round4_kernel():
     """Two launches give bitwise-equal outputs (fixed-order sums everywhere); the round-4 32-row
     kernel (agn_edge_bwd_fused, different MFMA k-order) agrees to bf16 rounding."""

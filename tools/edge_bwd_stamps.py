@@ -46,10 +46,13 @@ def main():
     core.proj_forward(N, x, spec.pack["proj"], spec.pack["proj_b"], P)
     de = torch.empty_like(e)
     g0 = torch.empty(E, H, dtype=dt, device=dev)
+    # DPD=1: with dP_d on the dW waves (the product default since round 5)
+    dpd = torch.empty(N, H, dtype=dt, device=dev) if os.environ.get("DPD", "1") == "1" else None
+    print(f"dP_d on the dW waves: {dpd is not None}")
 
     def run():
         return core.edge_bwd_fused(rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
-                                   src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de, g0=g0)
+                                   src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de, g0=g0, dpd=dpd, rowptr=lv.rowptr)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -93,7 +96,9 @@ def main():
         print("  phases (mean over waves): " + ", ".join(f"{p} {v / 4:.0f}" for p, v in zip(PHASES, tot)))
         for dwv in range(4):
             s = st[sel, 4 + dwv]
-            print(f"  dW wave {dwv}: waited {s[0, 0]} of {s[0, 1]} cycles ({s[0, 0] / max(s[0, 1], 1):.2f}), items {s[0, 2]}")
+            print(f"  dW wave {dwv}: waited {s[0, 0]} of {s[0, 1]} cycles ({s[0, 0] / max(s[0, 1], 1):.2f}), items {s[0, 2]}"
+                  + (f"; dP_d per L1 pair: G0 recompute {s[0, 3] / max(s[0, 2] / 6, 1):.0f}, walk "
+                     f"{s[0, 4] / max(s[0, 2] / 6, 1):.0f} cycles" if s[0, 3] else ""))
 
 
 if __name__ == "__main__":
