@@ -625,14 +625,16 @@ AGN_DEV int dpd_ids(const agn_edge_bwd_args& a, int tile, int lane) {
 }
 
 // one row of the walk: restart the sum at a new receiver, add the row, store the running sum.
-// A raw buffer store over the 64-byte slice dP_d[n][32d..32d+31]: lanes 32-63 address past its
-// end and are dropped by the range check, so the store needs no exec-mask branch (voff).
-AGN_DEV void dpd_row(const agn_edge_bwd_args& a, DpdWalk& st, int n, float v, int d, int voff) {
+// A raw buffer store: the descriptor (dpd_rsrc) spans the 64-byte slice dP_d[0][32d..32d+31], the
+// row is the SGPR offset n * 256 (outside the range check, which covers the VGPR offset only), and
+// lanes 32-63 address past the slice's end and are dropped, so the store needs no exec-mask branch.
+AGN_DEV __amdgpu_buffer_rsrc_t dpd_rsrc(const agn_edge_bwd_args& a, int d) {
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<bf16*>(a.dpd) + 32 * d, 0, 64, 0x00020000);
+}
+AGN_DEV void dpd_row(DpdWalk& st, int n, float v, __amdgpu_buffer_rsrc_t rs, int voff) {
   st.sum = (n != st.cur ? 0.f : st.sum) + v;
   st.cur = n;
-  bf16* rowp = reinterpret_cast<bf16*>(a.dpd) + ((size_t)n * H + 32 * d);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(rowp, 0, 64, 0x00020000);
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, (bf16)st.sum), rs, voff, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, (bf16)st.sum), rs, voff, n * (H * 2), 0);
 }
 
 // dP_d of a tile's L1 pair (ring slots k0, k1), then release() the slots. The ring reads stream
@@ -715,6 +717,7 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
   if (next_tile >= 0) st.dvn = dpd_ids(a, next_tile, lane);
   const int nval = min(32, a.rows - tile * 32);
   const int voff = hh ? 64 : 2 * c;  // dpd_row's store offset (lanes 32-63: dropped)
+  const __amdgpu_buffer_rsrc_t rs = dpd_rsrc(a, d);
   // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
   // lanes 0-31 take over by v_permlane32_swap, four registers at a time. Full tiles walk
   // straight-line code; only the last tile of the edge list checks its row count.
@@ -729,11 +732,11 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
     }
     if (nval == 32) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dpd_row(a, st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], d, voff);
+      for (int j = 0; j < 8; ++j) dpd_row(st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], rs, voff);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (8 * m + j < nval) dpd_row(a, st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], d, voff);
+        if (8 * m + j < nval) dpd_row(st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], rs, voff);
     }
     sched_fence();
   }
@@ -1013,7 +1016,8 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;
-  if (a->dpd && (!a->rowptr || a->nodes < 1 || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
+  // dpd_row's SGPR row offset n * 256 is 32-bit: nodes < 2^24
+  if (a->dpd && (!a->rowptr || a->nodes < 1 || a->nodes >= (1 << 24) || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
                  (reinterpret_cast<uintptr_t>(a->g0) & 15)))
     return AGN_E_ARG;
   hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
