@@ -28,6 +28,10 @@ class Seg(C.Structure):
                 ("ptr", vp), ("index", vp), ("store", vp)]
 
 
+# AGN_ACT_* (aerognn.h): the MLP hidden activation, mlp.py:37
+ACT = {"relu": 0, "gelu": 1, "silu": 2, "tanh": 3}
+
+
 class MlpFwdArgs(C.Structure):
     _fields_ = [("rows", i32), ("dtype", i32), ("hidden", i32), ("nlin", i32),
                 ("out_dim", i32), ("nseg", i32), ("use_ln", i32), ("out_ld", i32),
@@ -36,8 +40,8 @@ class MlpFwdArgs(C.Structure):
                 ("ln_g", vp), ("ln_b", vp),
                 ("proj", vp), ("src", vp), ("dst", vp),
                 ("resid", vp), ("out", vp),
-                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("_pad2", i32),
-                ("mask", vp * MAX_LIN)]
+                ("act", vp * MAX_LIN), ("hpre", vp), ("stats", vp), ("tiled", i32), ("act_fn", i32),
+                ("mask", vp * MAX_LIN), ("pre", vp * MAX_LIN)]
 
 
 class MlpBwdArgs(C.Structure):
@@ -50,7 +54,7 @@ class MlpBwdArgs(C.Structure):
                 ("din_nseg", i32), ("din_k", i32 * MAX_SEG),
                 ("din", vp * MAX_SEG), ("din_resid", i32 * MAX_SEG),
                 ("ln_partial", vp), ("tiled", i32), ("gpre_tiled", i32),
-                ("mask", vp * MAX_LIN)]
+                ("mask", vp * MAX_LIN), ("act_fn", i32), ("_pad3", i32), ("pre", vp * MAX_LIN)]
 
 
 MAX_WGRAD = 8
@@ -101,7 +105,8 @@ class F64Seg(C.Structure):
 class F64GemmArgs(C.Structure):
     _fields_ = [("rows", i32), ("n", i32), ("nseg", i32), ("_pad", i32), ("seg", F64Seg * 3), ("bias", vp),
                 ("add", vp * 2), ("add_idx", vp * 2), ("add_ld", i32 * 2), ("mask", vp), ("mask_ld", i32),
-                ("relu", i32), ("out", vp), ("out_ld", i32), ("_pad2", i32)]
+                ("relu", i32), ("out", vp), ("out_ld", i32), ("mask_act", i32), ("pre_out", vp),
+                ("pre_ld", i32), ("_pad3", i32)]
 
 
 class F64WgradArgs(C.Structure):

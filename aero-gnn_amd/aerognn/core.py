@@ -89,6 +89,11 @@ def _mask_of(t):
     return getattr(t, "agn_mask", None)
 
 
+def _pre_of(t):
+    """A non-ReLU activation's backward reads the saved pre-activation (attached by the allocator)."""
+    return getattr(t, "agn_pre", None)
+
+
 def is_tiled(t) -> bool:
     return t is not None and getattr(t, "agn_tiled", False)
 
@@ -209,10 +214,11 @@ class Pack:
 # ----------------------------------------------------------------------------- fused MLP chain
 def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out_ld=None,
                 ln=None, proj=None, src=None, dst=None, resid=None, acts=None, hpre=None, stats=None,
-                tag=None, cost=None):
-    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor)."""
+                tag=None, cost=None, act_fn=0):
+    """segs: list of (kind, k, ld, tensor, index_tensor, store_tensor); act_fn: AGN_ACT_* (L.ACT)."""
     a = L.MlpFwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
+    a.act_fn = act_fn
     a.out_dim, a.nseg = out_dim, len(segs)
     a.use_ln = 1 if ln is not None else 0
     a.out_ld = out_ld if out_ld is not None else out_dim
@@ -229,6 +235,7 @@ def mlp_forward(*, rows, dtype, hidden, nlin, out_dim, segs, wpk, bias, out, out
         for i, t in enumerate(acts):
             a.act[i] = ptr(t)
             a.mask[i] = ptr(_mask_of(t))
+            a.pre[i] = ptr(_pre_of(t))
     a.hpre, a.stats = ptr(hpre), ptr(stats)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))
     with timed(tag, cost):
@@ -262,10 +269,11 @@ def bwd_nblocks(rows):
 
 def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, gpre,
                  ln_g=None, hpre=None, stats=None, g2=None, gidx=None, din=(), ln_partial=None,
-                 tag=None, cost=None):
-    """din: list of (k, tensor_or_None, resid_flag)."""
+                 tag=None, cost=None, act_fn=0):
+    """din: list of (k, tensor_or_None, resid_flag); act_fn: the forward's AGN_ACT_*."""
     a = L.MlpBwdArgs()
     a.rows, a.dtype, a.hidden, a.nlin = rows, dt_code(dtype), hidden, nlin
+    a.act_fn = act_fn
     a.out_dim, a.in_dim = out_dim, in_dim
     a.use_ln = 1 if ln_g is not None else 0
     for i in range(nlin):
@@ -274,6 +282,7 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
     for i, t in enumerate(acts):
         a.act[i] = ptr(t)
         a.mask[i] = ptr(_mask_of(t))
+        a.pre[i] = ptr(_pre_of(t))
     a.hpre, a.stats, a.ln_g = ptr(hpre), ptr(stats), ln_g
     a.g, a.g2, a.gidx = ptr(g), ptr(g2), ptr(gidx)
     a.tiled = int(any(is_tiled(t) for t in list(acts or []) + [hpre]))

@@ -31,9 +31,12 @@ def _c(t):
     return t if t.is_contiguous() else t.contiguous()
 
 
-def gemm(rows, n, segs, out, bias=None, adds=(), mask=None, relu=False):
-    """out[rows][n] = relu?(mask?(sum over segs of A . B + bias + adds)). segs: (a, aidx, k, w,
-    transw) with B(j, c) = w[c][j] (transw) or w[j][c]; adds: (t, idx) addends [*, n]."""
+def gemm(rows, n, segs, out, bias=None, adds=(), mask=None, relu=False, act=None, mask_act=0, pre_out=None):
+    """out[rows][n] = f?(mask?(sum over segs of A . B + bias + adds)). segs: (a, aidx, k, w,
+    transw) with B(j, c) = w[c][j] (transw) or w[j][c]; adds: (t, idx) addends [*, n].
+    f: relu=True, or act = an AGN_ACT_* code (its pre-activation also to pre_out when given);
+    mask_act: 0 = ReLU backward on the saved activation `mask`, 1 + AGN_ACT_* = out *= f'(mask)
+    with `mask` the saved pre-activation."""
     if rows == 0:
         return out
     a = L.F64GemmArgs()
@@ -45,7 +48,9 @@ def gemm(rows, n, segs, out, bias=None, adds=(), mask=None, relu=False):
         a.add[q], a.add_idx[q], a.add_ld[q] = ptr(t), ptr(idx), t.stride(0)
     a.mask = ptr(mask)
     a.mask_ld = mask.stride(0) if mask is not None else 0
-    a.relu = int(relu)
+    a.mask_act = int(mask_act)
+    a.relu = 1 + int(act) if act is not None else int(relu)
+    a.pre_out, a.pre_ld = ptr(pre_out), pre_out.stride(0) if pre_out is not None else 0
     a.out, a.out_ld = ptr(out), out.stride(0)
     check(L.lib().agn_f64_gemm(C.byref(a), stream()), "f64_gemm")
     return out
@@ -73,10 +78,11 @@ def scatter_rows_sum(d, idx, nrows):
 
 
 class Chain:
-    """A Linear / ReLU chain + optional LayerNorm bound to fp64 parameters: lins = [(W, b), ...]."""
+    """A Linear / activation chain + optional LayerNorm bound to fp64 parameters: lins = [(W, b), ...],
+    act = the AGN_ACT_* code between the Linears (mlp.py:37)."""
 
-    def __init__(self, lins, ln=None, eps=1e-5):
-        self.lins, self.ln, self.eps = lins, ln, eps
+    def __init__(self, lins, ln=None, eps=1e-5, act=0):
+        self.lins, self.ln, self.eps, self.act = lins, ln, eps, act
 
     def params(self):
         out = []
@@ -103,21 +109,28 @@ class MLP64Fn(torch.autograd.Function):
         xs = [_c(x) for x in xs]
         dev = xs[0].device
         nl = len(chain.lins)
-        acts, z = [], None
+        relu = chain.act == L.ACT["relu"]
+        acts, pres, z = [], [], None
         for l, (w, b) in enumerate(chain.lins):
             n = w.shape[0]
             o = torch.empty(rows, n, dtype=F64, device=dev)
+            hid = l < nl - 1
+            # hidden layers: the activation in the epilogue; a non-ReLU one also keeps its input
+            kw = {} if not hid else ({"relu": True} if relu else
+                                     {"act": chain.act, "pre_out": torch.empty(rows, n, dtype=F64, device=dev)})
             if l == 0:
                 segs, k0 = [], 0
                 for x, idx in zip(xs, idxs):
                     k = x.shape[1]
                     segs.append((x, idx, k, w[:, k0:k0 + k], 1))
                     k0 += k
-                gemm(rows, n, segs, o, bias=b, adds=[(_c(t), i) for t, i in zip(adds, add_idx)], relu=l < nl - 1)
+                gemm(rows, n, segs, o, bias=b, adds=[(_c(t), i) for t, i in zip(adds, add_idx)], **kw)
             else:
-                gemm(rows, n, [(acts[-1], None, acts[-1].shape[1], w, 1)], o, bias=b, relu=l < nl - 1)
-            if l < nl - 1:
+                gemm(rows, n, [(acts[-1], None, acts[-1].shape[1], w, 1)], o, bias=b, **kw)
+            if hid:
                 acts.append(o)
+                if not relu:
+                    pres.append(kw["pre_out"])
             else:
                 z = o
         mean = rstd = None
@@ -139,7 +152,7 @@ class MLP64Fn(torch.autograd.Function):
         ctx.meta = meta
         ctx.nsrc = [x.shape[0] for x in xs]
         ctx.nadd = [t.shape[0] for t in adds]
-        ctx.save_for_backward(*xs, *acts, z, *([mean, rstd] if chain.ln is not None else []))
+        ctx.save_for_backward(*xs, *acts, z, *([mean, rstd] if chain.ln is not None else []), *pres)
         return y
 
     @staticmethod
@@ -150,6 +163,8 @@ class MLP64Fn(torch.autograd.Function):
         xs = saved[:ns]
         acts = list(saved[ns:ns + nl - 1])
         z = saved[ns + nl - 1]
+        relu = chain.act == L.ACT["relu"]
+        pres = [] if relu else list(saved[len(saved) - (nl - 1):])
         gy = _c(gy)
         dev = gy.device
         pgrads = []
@@ -180,8 +195,13 @@ class MLP64Fn(torch.autograd.Function):
                 a_in = acts[l - 1]
                 wgrad(dz, a_in, None, dw, dbias)
                 d_in = torch.empty(rows, w.shape[1], dtype=F64, device=dev)
-                # ReLU backward on the saved activation: d(pre) = (dz W) . [a_in > 0]
-                gemm(rows, w.shape[1], [(dz, None, w.shape[0], w, 0)], d_in, mask=a_in)
+                # the activation's backward: ReLU on the saved activation, d(pre) = (dz W) . [a_in > 0];
+                # others at the saved pre-activation, d(pre) = (dz W) . f'(pre)
+                if relu:
+                    gemm(rows, w.shape[1], [(dz, None, w.shape[0], w, 0)], d_in, mask=a_in)
+                else:
+                    gemm(rows, w.shape[1], [(dz, None, w.shape[0], w, 0)], d_in, mask=pres[l - 1],
+                         mask_act=1 + chain.act)
                 lin_grads[l] = (dw, dbias)
                 dz = d_in
             else:
@@ -275,8 +295,8 @@ def _ln_of(mlp_module):
 
 
 def _check_mlp(m):
-    if m.activation_fn != "relu":
-        raise NotImplementedError("aerognn float64 MLP implements activation_fn='relu' (config.yaml)")
+    if m.activation_fn not in L.ACT:
+        raise NotImplementedError(f"aerognn float64 MLP implements activation_fn in {sorted(L.ACT)}")
     if m.training and m.dropout.p > 0:
         raise NotImplementedError("aerognn float64 MLP: dropout > 0 in training is not implemented")
 
@@ -284,7 +304,8 @@ def _check_mlp(m):
 def mlp_chain(m):
     """models/mlp.py MLP -> Chain (the reference's layer list, mlp.py:21-35)."""
     _check_mlp(m)
-    return Chain([(l.weight, l.bias) for l in m.layers], _ln_of(m), m.layer_norm.eps if m.use_layer_norm else 1e-5)
+    return Chain([(l.weight, l.bias) for l in m.layers], _ln_of(m), m.layer_norm.eps if m.use_layer_norm else 1e-5,
+                 act=L.ACT[m.activation_fn])
 
 
 def mlp_forward(m, x, rows=None):

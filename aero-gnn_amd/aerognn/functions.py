@@ -43,13 +43,16 @@ def _ln_grads(partial, nblk, M, dtype):
 
 # --------------------------------------------------------------------------- chain specs
 class ChainSpec:
-    """A Linear/ReLU chain + optional LayerNorm, bound to nn.Parameters.
+    """A Linear/activation chain + optional LayerNorm, bound to nn.Parameters.
 
     linears: list of (weight, bias_or_None) in order; ln: (gamma, beta) or None.
     Pack keys: W{l} (A = W_l), T{l} (A = W_l^T), b{l}, ln_g, ln_b.
     """
 
-    def __init__(self, linears, ln, hidden, pack: Pack, prefix=""):
+    def __init__(self, linears, ln, hidden, pack: Pack, prefix="", act="relu"):
+        if act not in L.ACT:
+            raise NotImplementedError(f"aerognn MLP kernels implement activation_fn in {sorted(L.ACT)}, got {act!r}")
+        self.act = L.ACT[act]  # AGN_ACT_* between the Linears (mlp.py:37)
         self.linears = linears
         self.ln = ln
         self.hidden = hidden
@@ -108,8 +111,11 @@ def _alloc_saves(spec, rows, dtype, dev, train):
         return None, None, None
     emp = tiled_empty if spec.tiled_saves else (lambda r, w, dt, d: torch.empty(r, w, dtype=dt, device=d))
     acts = [emp(rows, spec.hidden, dtype, dev) for _ in range(spec.nlin - 1)]
-    for t in acts:  # sign bits for the backward (AGN_RELU_MASK); the rows stay for agn_wgrad
-        t.agn_mask = relu_mask_empty(rows, spec.hidden, dev)
+    for t in acts:  # what the activation's backward reads; the rows themselves stay for agn_wgrad
+        if spec.act == L.ACT["relu"]:
+            t.agn_mask = relu_mask_empty(rows, spec.hidden, dev)  # sign bits (AGN_RELU_MASK)
+        else:
+            t.agn_pre = emp(rows, spec.hidden, dtype, dev)  # the pre-activation (agn_mlp_fwd_args.pre)
     hpre = stats = None
     if spec.ln is not None:
         hpre = emp(rows, spec.out_dim, dtype, dev)
@@ -200,7 +206,7 @@ class MLPFn(torch.autograd.Function):
             segs = [(L.SEG_GATHER, k, x.stride(0), x[:, k0:], idx, None) for k0, k in ks]
         else:
             segs = [(L.SEG_PLAIN, k, x.stride(0), x[:, k0:], None, None) for k0, k in ks]
-        mlp_forward(rows=nrow, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+        mlp_forward(rows=nrow, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, act_fn=spec.act, out_dim=spec.out_dim,
                     segs=segs, wpk=spec.wpk(), bias=spec.biases(), ln=spec.lnp(), out=out,
                     acts=acts, hpre=hpre, stats=stats)
         ctx.spec, ctx.idx, ctx.nrow = spec, idx, nrow
@@ -221,7 +227,7 @@ class MLPFn(torch.autograd.Function):
         dparts = [torch.empty(rows, k, dtype=dt, device=x.device) if need_dx else None for _, k in ks]
         nblk = bwd_nblocks(rows)
         part = torch.empty(nblk, 2 * spec.out_dim, dtype=torch.float32, device=x.device) if spec.ln else None
-        nblk = mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, out_dim=spec.out_dim,
+        nblk = mlp_backward(rows=rows, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, act_fn=spec.act, out_dim=spec.out_dim,
                             in_dim=spec.in_dim, wtpk=spec.wtpk(), acts=ctx.acts or [], g=gy, gpre=gpre,
                             ln_g=spec.lnp()[0] if spec.ln else None, hpre=ctx.hpre, stats=ctx.stats,
                             din=[(k, d, False) for (_, k), d in zip(ks, dparts)], ln_partial=part)
@@ -296,7 +302,7 @@ class LayerSpec:
             H = nbm.layers[0].weight.shape[0]
             self.node = ChainSpec([(m.weight, m.bias) for m in nbm.layers],
                                   (nbm.layer_norm.weight, nbm.layer_norm.bias) if nbm.use_layer_norm else None,
-                                  H, self.pack, "n")
+                                  H, self.pack, "n", act=nbm.activation_fn)
         if edge_block is not None:
             eb = edge_block
             self.trick = hasattr(eb, "edge_lin")
@@ -320,9 +326,8 @@ class LayerSpec:
                 H = em.layers[0].weight.shape[0] if H is None else H
                 self.edge = ChainSpec([(m.weight, m.bias) for m in em.layers],
                                       (em.layer_norm.weight, em.layer_norm.bias) if em.use_layer_norm else None,
-                                      H, self.pack, "e")
-            if getattr(eb.mlp, "activation_fn", "relu") != "relu":
-                raise NotImplementedError("aerognn kernels implement ReLU MLPs (config.yaml activation_fn)")
+                                      H, self.pack, "e", act=em.activation_fn)
+            # (EdgeBlockSum's chain is ReLU whatever activation_fn says: mgnLayer.py:81)
         self.H = H
         if H not in (32, 64, 128):
             raise NotImplementedError(f"aerognn kernels support hidden 32/64/128, got {H}")
@@ -333,8 +338,6 @@ class LayerSpec:
                     raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
         if self.node is not None and self.node.in_dim != 2 * H:
             raise NotImplementedError("aerognn GMP kernels need node_dim == edge_dim == hidden_dim")
-        if node_block is not None and node_block.mlp.activation_fn != "relu":
-            raise NotImplementedError("aerognn kernels implement ReLU MLPs (config.yaml activation_fn)")
 
     @classmethod
     def from_gmp(cls, gmp):
@@ -343,15 +346,19 @@ class LayerSpec:
         self = cls.__new__(cls)
         self.pack = Pack()
         self.trick, self.gmp_order, self.aggregation = False, True, "add"
-        if not isinstance(gmp.edge_mlp[1], torch.nn.ReLU):
-            raise NotImplementedError("aerognn kernels implement ReLU MLPs (GMP activation='relu')")
+        acts = {torch.nn.ReLU: "relu", torch.nn.SiLU: "silu", torch.nn.GELU: "gelu", torch.nn.Tanh: "tanh"}
+        ea, na = acts.get(type(gmp.edge_mlp[1])), acts.get(type(gmp.node_mlp[1]))
+        if ea is None or na is None or (isinstance(gmp.edge_mlp[1], torch.nn.GELU) and gmp.edge_mlp[1].approximate != "none"):
+            raise NotImplementedError("aerognn GMP kernels implement ReLU / SiLU / GELU / Tanh MLPs")
         e0, e2, eln = gmp.edge_mlp[0], gmp.edge_mlp[2], gmp.edge_mlp[3]
         n0, n2, nln = gmp.node_mlp[0], gmp.node_mlp[2], gmp.node_mlp[3]
         H = e0.weight.shape[0]
         if H not in (32, 64, 128):
             raise NotImplementedError(f"aerognn kernels support hidden 32/64/128, got {H}")
-        self.edge = ChainSpec([(e0.weight, e0.bias), (e2.weight, e2.bias)], (eln.weight, eln.bias), H, self.pack, "e")
-        self.node = ChainSpec([(n0.weight, n0.bias), (n2.weight, n2.bias)], (nln.weight, nln.bias), H, self.pack, "n")
+        self.edge = ChainSpec([(e0.weight, e0.bias), (e2.weight, e2.bias)], (eln.weight, eln.bias), H, self.pack, "e",
+                              act=ea)
+        self.node = ChainSpec([(n0.weight, n0.bias), (n2.weight, n2.bias)], (nln.weight, nln.bias), H, self.pack, "n",
+                              act=na)
         self.H = H
         for c in (self.edge, self.node):
             c.check_hidden()
@@ -421,7 +428,7 @@ class GMPFn(torch.autograd.Function):
                              tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
                                                                                                  False)))
             else:
-                mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+                mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H,
                             segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
                             wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), proj=P, src=level.src, dst=level.dst,
                             resid=e, out=e_out, acts=ea, hpre=ehp, stats=est,
@@ -431,7 +438,7 @@ class GMPFn(torch.autograd.Function):
             se = (L.SEG_PLAIN, H, e.stride(0), e, None, None)
             ss = (L.SEG_GATHER, H, x.stride(0), x, level.src, None)
             sd = (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)
-            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H,
+            mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H,
                         segs=[ss, sd, se] if spec.gmp_order else [se, ss, sd],
                         wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), resid=e, out=e_out,
                         acts=ea, hpre=ehp, stats=est,
@@ -444,7 +451,7 @@ class GMPFn(torch.autograd.Function):
         kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
         agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
         aseg = (kind, H, e_out.stride(0), e_out, level.rowptr, agg)
-        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
+        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, act_fn=ns.act, out_dim=H,
                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None), aseg],
                     wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), resid=x, out=x_out,
                     acts=na, hpre=nhp, stats=nst,
@@ -476,7 +483,7 @@ class GMPFn(torch.autograd.Function):
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb_n = bwd_nblocks(N)
         part_n = torch.empty(nb_n, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
-        nb_n = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+        nb_n = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, act_fn=ns.act, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=gx, gpre=gpre_n, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
                      din=[(H, dx, True), (H, dagg, False)], ln_partial=part_n,
                      tag="node_bwd", cost=with_alg(alg8d_node(N, H, x.element_size(), bwd=True, proj=spec.trick),
@@ -507,7 +514,7 @@ class GMPFn(torch.autograd.Function):
                 dxd = torch.empty(E, H, dtype=dt, device=dev)
                 din = [(H, dxs, False), (H, dxd, False), (H, de, True)] if spec.gmp_order else \
                     [(H, de, True), (H, dxs, False), (H, dxd, False)]
-            nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim,
+            nb_e = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H, in_dim=es.in_dim,
                                 wtpk=es.wtpk(), acts=ea, g=ge, g2=dagg, gidx=lv.dst, gpre=gpre_e,
                                 ln_g=es.lnp()[0] if es.ln else None, hpre=ehp, stats=est, din=din, ln_partial=part_e,
                                 tag="edge_bwd",
@@ -700,7 +707,7 @@ class EdgeBlockFn(torch.autograd.Function):
             segs = [(L.SEG_PLAIN, H, e.stride(0), e, None, None),
                     (L.SEG_GATHER, H, x.stride(0), x, level.src, None),
                     (L.SEG_GATHER, H, x.stride(0), x, level.dst, None)]
-        mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, segs=segs, wpk=es.wpk(),
+        mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H, segs=segs, wpk=es.wpk(),
                     bias=es.biases(), ln=es.lnp(), proj=P, src=level.src if P is not None else None,
                     dst=level.dst if P is not None else None, out=out, acts=ea, hpre=ehp, stats=est)
         ctx.spec, ctx.level, ctx.saves = spec, level, (ea, ehp, est)
@@ -726,7 +733,7 @@ class EdgeBlockFn(torch.autograd.Function):
             dxs = torch.empty(E, H, dtype=dt, device=dev)
             dxd = torch.empty(E, H, dtype=dt, device=dev)
             din = [(H, de, False), (H, dxs, False), (H, dxd, False)]
-        nb = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
+        nb = mlp_backward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H, in_dim=es.in_dim, wtpk=es.wtpk(),
                      acts=ea, g=g, gpre=gpre, ln_g=es.lnp()[0] if es.ln else None, hpre=ehp, stats=est,
                      din=din, ln_partial=part)
         if spec.trick:
@@ -768,7 +775,7 @@ class NodeBlockFn(torch.autograd.Function):
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         agg = torch.empty(N, H, dtype=dt, device=dev) if train else None
         kind = L.SEG_MEAN if spec.aggregation == "mean" else L.SEG_SUM
-        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H,
+        mlp_forward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, act_fn=ns.act, out_dim=H,
                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None),
                           (kind, H, e.stride(0), e, level.rowptr, agg)],
                     wpk=ns.wpk(), bias=ns.biases(), ln=ns.lnp(), out=out, acts=na, hpre=nhp, stats=nst)
@@ -790,7 +797,7 @@ class NodeBlockFn(torch.autograd.Function):
         dagg = torch.empty(N, H, dtype=dt, device=dev)
         nb = bwd_nblocks(N)
         part = torch.empty(nb, 2 * H, dtype=torch.float32, device=dev) if ns.ln else None
-        nb = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
+        nb = mlp_backward(rows=N, dtype=dt, hidden=H, nlin=ns.nlin, act_fn=ns.act, out_dim=H, in_dim=2 * H, wtpk=ns.wtpk(),
                      acts=na, g=g, gpre=gpre, ln_g=ns.lnp()[0] if ns.ln else None, hpre=nhp, stats=nst,
                      din=[(H, dx, False), (H, dagg, False)], ln_partial=part)
         de = torch.empty_like(e)

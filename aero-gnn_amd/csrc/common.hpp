@@ -14,6 +14,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "aerognn.h"
 
 typedef __bf16 bf16;
 typedef bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -128,6 +129,35 @@ template <> AGN_DEV float lo16<bf16>(uint32_t u) { return lo_bf16(u); }
 template <> AGN_DEV float hi16<bf16>(uint32_t u) { return hi_bf16(u); }
 template <> AGN_DEV float lo16<f16>(uint32_t u) { return (float)__builtin_bit_cast(f16x2, u)[0]; }
 template <> AGN_DEV float hi16<f16>(uint32_t u) { return (float)__builtin_bit_cast(f16x2, u)[1]; }
+
+// ---------------------------------------------------------------- MLP hidden activations
+// (AGN_ACT_*, mlp.py:37 getattr(F, activation_fn)). fp32 forms of torch's kernels: F.gelu with
+// approximate='none', F.silu, torch.tanh; their backward formulas are torch's GeluBackward,
+// SiluBackward (from the input) and TanhBackward (from the output, rounded as the forward stored it).
+AGN_DEV float act_fwd(int k, float x) {
+  if (k == AGN_ACT_GELU) return x * 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+  if (k == AGN_ACT_SILU) return x / (1.f + expf(-x));
+  if (k == AGN_ACT_TANH) return tanhf(x);
+  return fmaxf(x, 0.f);
+}
+// dy * f'(x), x the (rounded) pre-activation, dy the gradient of the (rounded) output
+template <typename T>
+AGN_DEV float act_bwd(int k, float x, float dy) {
+  if (k == AGN_ACT_GELU) {
+    const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752440f));
+    const float pdf = expf(-0.5f * x * x) * 0.39894228040143267794f;  // M_2_SQRTPI * M_SQRT1_2 / 2
+    return dy * (cdf + x * pdf);
+  }
+  if (k == AGN_ACT_SILU) {
+    const float s = 1.f / (1.f + expf(-x));
+    return dy * s * (1.f + x * (1.f - s));
+  }
+  if (k == AGN_ACT_TANH) {
+    const float y = round_t<T>(tanhf(x));
+    return dy * (1.f - y * y);
+  }
+  return x > 0.f ? dy : 0.f;
+}
 
 // o[0..3] = features 16i+4h.., o[4..7] = 16i+8+4h.. (acc registers 8i..8i+7)
 AGN_DEV void load8_w(float (&o)[8], const bf16* rowp, int i, int h) {

@@ -22,6 +22,30 @@ constexpr int GT = 64;   // output tile edge
 constexpr int GK = 16;   // k chunk
 constexpr int GTHR = 256;
 
+// MLP hidden activations in float64 (AGN_ACT_*; torch's formulas, as common.hpp act_fwd / act_bwd)
+AGN_DEV double act_fwd64(int k, double x) {
+  if (k == AGN_ACT_GELU) return x * 0.5 * (1.0 + erf(x * 0.70710678118654752440));
+  if (k == AGN_ACT_SILU) return x / (1.0 + exp(-x));
+  if (k == AGN_ACT_TANH) return tanh(x);
+  return x > 0.0 ? x : 0.0;
+}
+AGN_DEV double act_bwd64(int k, double x, double dy) {
+  if (k == AGN_ACT_GELU) {
+    const double cdf = 0.5 * (1.0 + erf(x * 0.70710678118654752440));
+    const double pdf = exp(-0.5 * x * x) * 0.39894228040143267794;
+    return dy * (cdf + x * pdf);
+  }
+  if (k == AGN_ACT_SILU) {
+    const double sg = 1.0 / (1.0 + exp(-x));
+    return dy * sg * (1.0 + x * (1.0 - sg));
+  }
+  if (k == AGN_ACT_TANH) {
+    const double y = tanh(x);
+    return dy * (1.0 - y * y);
+  }
+  return x > 0.0 ? dy : 0.0;
+}
+
 __global__ __launch_bounds__(GTHR) void f64_gemm_kernel(const agn_f64_gemm_args a) {
   __shared__ double As[GK][GT + 1];
   __shared__ double Bs[GK][GT + 1];
@@ -86,8 +110,17 @@ __global__ __launch_bounds__(GTHR) void f64_gemm_kernel(const agn_f64_gemm_args 
           const long ar = a.add_idx[q] ? a.add_idx[q][row] : row;
           v += a.add[q][ar * (long)a.add_ld[q] + n];
         }
-      if (a.mask && !(a.mask[(long)row * a.mask_ld + n] > 0.0)) v = 0.0;
-      if (a.relu) v = v > 0.0 ? v : 0.0;
+      if (a.mask) {
+        const double m = a.mask[(long)row * a.mask_ld + n];
+        if (a.mask_act == 0) {
+          if (!(m > 0.0)) v = 0.0;  // ReLU backward on the saved activation
+        } else {
+          v = act_bwd64(a.mask_act - 1, m, v);  // f'(pre-activation)
+        }
+      }
+      if (a.pre_out) a.pre_out[(long)row * a.pre_ld + n] = v;
+      if (a.relu == 1) v = v > 0.0 ? v : 0.0;
+      else if (a.relu > 1) v = act_fwd64(a.relu - 1, v);
       a.out[(long)row * a.out_ld + n] = v;
     }
   }

@@ -208,7 +208,28 @@ AGN_DEV void walk2_segment(float (&in)[NR], const agn_seg& s, int rr, bool valid
   if (s.store) store_row<bf16, NR, true>(reinterpret_cast<bf16*>(s.store) + (size_t)rr * s.k, s.k, in, h, valid);
 }
 
-template <typename T, int NT, int MODE>
+// A hidden activation other than ReLU (AGN_ACT_*): the Linear output rounded to T, saved to pre
+// (the backward's x) when given, the activation applied in fp32 and packed (rounded) into b
+template <typename T, int NT, int NR>
+AGN_DEV void set_act(BOp<T, NR>& b, const f32x16 (&acc)[NT], int k, T* pre, int tiled, int row, int h, bool valid) {
+  constexpr int H = 32 * NT;
+  float v[NR];
+#pragma unroll
+  for (int i = 0; i < NR; ++i) v[i] = round_t<T>(acc[i / 16][i % 16]);
+  if (pre) {
+    BOp<T, NR> pb;
+    pb.set(v);
+    if (tiled) pb.store_tiled(pre, row, h, valid);
+    else pb.store(pre + (size_t)row * H, h, valid);
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i) v[i] = act_fwd(k, v[i]);
+  b.set(v);
+}
+
+// GACT: a hidden activation other than ReLU (agn_mlp_*_args.act_fn); the ReLU instantiations
+// carry none of its registers
+template <typename T, int NT, int MODE, bool GACT>
 __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_args a) {
   constexpr int H = 32 * NT;
   constexpr int NR = 16 * NT;
@@ -313,13 +334,15 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_fwd_kernel(const agn_mlp_fwd_arg
       const int otn = (outl + 31) / 32;
       __syncthreads();
       stage_block(wl, a.wpk[l], NUH, 0, otn, 0, NUH);
-      b.template set_relu<NT>(acc);
+      if constexpr (GACT) set_act<T, NT, NR>(b, acc, a.act_fn, reinterpret_cast<T*>(a.pre[l - 1]), a.tiled, row, h, valid);
+      else b.template set_relu<NT>(acc);
       if (a.act[l - 1]) {
         if (a.tiled) b.store_tiled(reinterpret_cast<T*>(a.act[l - 1]), row, h, valid);
         else b.store(reinterpret_cast<T*>(a.act[l - 1]) + (size_t)row * H, h, valid);
       }
       // waves past the last 32-row tile (the grid rounds up to WPB waves) own no mask tile
-      if (a.mask[l - 1] && wave * 32 < a.rows) store_relu_mask<T, NR>(a.mask[l - 1], b, wave, lane);
+      if (!GACT && a.mask[l - 1] && wave * 32 < a.rows)
+        store_relu_mask<T, NR>(a.mask[l - 1], b, wave, lane);
       if (OUT_FULL || !last) acc_bias<NT, true>(acc, a.bias[l], H, h);
       else acc_bias<NT, false>(acc, a.bias[l], outl, h);
       __syncthreads();
@@ -447,7 +470,9 @@ AGN_DEV void load_grad(float (&g)[NR], const agn_mlp_bwd_args& a, int rr, bool v
   }
 }
 
-template <typename T, int NT, int MODE>
+// GACT: a hidden activation other than ReLU (agn_mlp_*_args.act_fn); the ReLU instantiations
+// carry none of its registers
+template <typename T, int NT, int MODE, bool GACT>
 __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_args a) {
   constexpr bool VEC = (MODE == M_VEC);
   constexpr int H = 32 * NT;
@@ -554,11 +579,23 @@ __global__ __launch_bounds__(BLOCK, 2) void mlp_bwd_kernel(const agn_mlp_bwd_arg
       gemm<T, NT, NR, true>(acc, b, kuM, wl, kuM, NT, lane);
       cbarrier();
       acc_to_regs<NT, NR>(A, acc);
-      // AGN_RELU_MASK sign bits (8 B per lane instead of the activation row)
-      uint32_t mk[mask_dwords<NR>()];
-      load_relu_mask<NR>(mk, a.mask[l - 1], min(wave, (a.rows - 1) / 32), lane);  // clamp: idle waves
+      if constexpr (!GACT) {
+        // AGN_RELU_MASK sign bits (8 B per lane instead of the activation row)
+        uint32_t mk[mask_dwords<NR>()];
+        load_relu_mask<NR>(mk, a.mask[l - 1], min(wave, (a.rows - 1) / 32), lane);  // clamp: idle waves
 #pragma unroll
-      for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, A[i]);
+        for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, A[i]);
+      } else {
+        // dL/dy rounded to T (the Linear backward's output in the storage type), times f'(x) at
+        // the forward's saved pre-activation x
+        const T* pb = reinterpret_cast<const T*>(a.pre[l - 1]);
+#pragma unroll
+        for (int q = 0; q < NR / 4; ++q) {
+          const f32x4 x = a.tiled ? load4_tiled<T, NR>(pb, q, rr, h) : load4(pb + (size_t)rr * H + 8 * q + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) A[4 * q + e] = act_bwd<T>(a.act_fn, x[e], round_t<T>(A[4 * q + e]));
+        }
+      }
     } else {
       int koff = 0;
       for (int s = 0; s < a.din_nseg; ++s) {
@@ -1144,8 +1181,13 @@ inline int launch_status() {
 
 }  // namespace
 
-#define AGN_LAUNCH(KERNEL, T, NT, MODE) \
-  hipLaunchKernelGGL((KERNEL<T, NT, MODE>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a)
+#define AGN_LAUNCH(KERNEL, T, NT, MODE)                                                              \
+  do {                                                                                                \
+    if (a->act_fn != AGN_ACT_RELU)                                                                    \
+      hipLaunchKernelGGL((KERNEL<T, NT, MODE, true>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a);  \
+    else                                                                                              \
+      hipLaunchKernelGGL((KERNEL<T, NT, MODE, false>), grid, dim3(BLOCK), 0, (hipStream_t)stream, *a); \
+  } while (0)
 
 #define AGN_FWD_MODES(T, NT)                                   \
   switch (mode) {                                              \
@@ -1215,7 +1257,7 @@ bool bwd_ptrs_aligned(const agn_mlp_bwd_args* a) {
 }
 int g_opt_resident = 1;
 bool res_fwd_ok(const agn_mlp_fwd_args* a, bool vec) {
-  return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
+  return g_opt_resident && vec && a->act_fn == AGN_ACT_RELU && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->nseg == 1 &&
          a->seg[0].kind == AGN_SEG_PLAIN && a->seg[0].k == 128 && a->out_dim == 128 && a->out_ld == 128 &&
          a->seg[0].ld % 8 == 0 && a->rows >= 64 * 1024;
 }
@@ -1226,8 +1268,8 @@ bool res_bwd_ok(const agn_mlp_bwd_args* a, bool vec) {
   // nlin == 1 with LayerNorm and no dX: the LayerNorm backward alone (G3 for agn_edge_bwd_fused)
   const bool din_ok = need_dx ? (a->din_nseg == 1 && a->in_dim == 128 && a->din_k[0] == 128)
                               : (a->nlin > 1 || a->use_ln);
-  return g_opt_resident && vec && a->dtype == AGN_BF16 && a->hidden == 128 && a->nlin <= RES_MAXL && a->out_dim == 128 &&
-         din_ok && a->rows >= 64 * 1024;
+  return g_opt_resident && vec && a->act_fn == AGN_ACT_RELU && a->dtype == AGN_BF16 && a->hidden == 128 &&
+         a->nlin <= RES_MAXL && a->out_dim == 128 && din_ok && a->rows >= 64 * 1024;
 }
 }  // namespace
 
@@ -1292,8 +1334,9 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   }
   if (a->nlin > 1 && a->out_dim > a->hidden) return AGN_E_SHAPE;
   if (a->use_ln && a->out_dim > a->hidden) return AGN_E_SHAPE;
+  if (a->act_fn < AGN_ACT_RELU || a->act_fn > AGN_ACT_TANH) return AGN_E_ARG;
   for (int l = 0; l < a->nlin; ++l)
-    if (!al16(a->act[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
+    if (!al16(a->act[l]) || !al16(a->pre[l])) return AGN_E_ARG;  // activation buffers are always 16-B accessed
   int mode = M_GEN;
   if (fwd_ptrs_aligned(a)) {
     if (in_full && out_full) mode = M_VEC;
@@ -1322,8 +1365,12 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
     if (a->din_k[s] > a->hidden) return AGN_E_SHAPE;
     if (s + 1 < a->din_nseg && (a->din_k[s] % 32) != 0) return AGN_E_SHAPE;
   }
-  for (int l = 0; l + 1 < a->nlin; ++l)
-    if (!a->mask[l]) return AGN_E_ARG;  // the ReLU backward reads the sign bits (AGN_RELU_MASK)
+  if (a->act_fn < AGN_ACT_RELU || a->act_fn > AGN_ACT_TANH) return AGN_E_ARG;
+  for (int l = 0; l + 1 < a->nlin; ++l) {
+    // the ReLU backward reads the sign bits (AGN_RELU_MASK), the others the saved pre-activation
+    if (a->act_fn == AGN_ACT_RELU ? !a->mask[l] : (!a->pre[l] || !al16(a->pre[l]))) return AGN_E_ARG;
+    if (a->act_fn != AGN_ACT_RELU && a->tiled == 0 && a->hidden % 4) return AGN_E_SHAPE;
+  }
   int mode = M_GEN;
   if (bwd_ptrs_aligned(a)) {
     if (a->out_dim == a->hidden) mode = M_VEC;

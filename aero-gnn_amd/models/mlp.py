@@ -37,14 +37,12 @@ class MLP(nn.Module):
 
     def spec(self):
         if self._spec is None:
-            if self.activation_fn != 'relu':
-                raise NotImplementedError("aerognn fused MLP implements activation_fn='relu' (config.yaml)")
             H = self.hidden_dim if len(self.layers) > 1 else max(32, ((self.layers[0].weight.shape[0] + 31) // 32) * 32)
             if H not in (32, 64, 128):
                 raise NotImplementedError(f"aerognn fused MLP supports hidden_dim 32/64/128, got {H}")
             lins = [(m.weight, m.bias) for m in self.layers]
             ln = (self.layer_norm.weight, self.layer_norm.bias) if self.use_layer_norm else None
-            self._spec = ChainSpec(lins, ln, H, Pack())
+            self._spec = ChainSpec(lins, ln, H, Pack(), act=self.activation_fn)
             self._spec.check_hidden()
         return self._spec
 

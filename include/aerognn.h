@@ -39,6 +39,10 @@ extern "C" {
 enum { AGN_F32 = 0, AGN_BF16 = 1, AGN_F16 = 2, AGN_F64 = 3 };  /* F64: graph ops and the agn_f64_* entries */
 enum { AGN_SEG_PLAIN = 0, AGN_SEG_GATHER = 1, AGN_SEG_SUM = 2, AGN_SEG_MEAN = 3 };
 enum { AGN_E_ARG = -1, AGN_E_DTYPE = -2, AGN_E_HIDDEN = -3, AGN_E_SHAPE = -4 };
+/* The MLP's hidden activation (mlp.py:37 getattr(F, activation_fn)): ReLU, GELU (exact erf form,
+ * F.gelu's default), SiLU, tanh. For 16-bit storage the Linear output is rounded first and the
+ * activation applied to the rounded value in fp32, then rounded (the bf16 module's order). */
+enum { AGN_ACT_RELU = 0, AGN_ACT_GELU = 1, AGN_ACT_SILU = 2, AGN_ACT_TANH = 3 };
 
 /* One input segment of a concatenated MLP input row (torch.cat in mgnLayer.py:44,151).
  * PLAIN : row r of ptr;  GATHER: row index[r] of ptr (x[row], x[col] of mgnLayer.py:40-41);
@@ -79,8 +83,10 @@ typedef struct {
   void* hpre;                      /* last Linear output before LN, [rows][out_dim] */
   float* stats;                    /* [rows][2] = mean, rstd */
   int tiled;                       /* 1: act/hpre in the tiled layout (AGN_TILED below, hidden-wide) */
-  int _pad2;
-  void* mask[AGN_MAX_LIN];         /* optional AGN_RELU_MASK of act[l] (may be given without act[l]) */
+  int act_fn;                      /* AGN_ACT_* between the Linears (0 = ReLU) */
+  void* mask[AGN_MAX_LIN];         /* optional AGN_RELU_MASK of act[l] (may be given without act[l]; ReLU only) */
+  void* pre[AGN_MAX_LIN];          /* optional (act_fn != ReLU, training): the rounded Linear output of
+                                      hidden layer l before the activation, laid out as act[l] */
 } agn_mlp_fwd_args;
 
 typedef struct {
@@ -111,7 +117,10 @@ typedef struct {
   float* ln_partial;               /* [agn_mlp_bwd_nwaves(rows)][2][out_dim]: sum g*xhat, sum g */
   int tiled;                       /* 1: act/hpre are read in the tiled layout */
   int gpre_tiled;                  /* bit l: gpre[l] written in the tiled layout (hidden-wide only) */
-  const void* mask[AGN_MAX_LIN];   /* AGN_RELU_MASK of hidden layer l < nlin-1 (required) */
+  const void* mask[AGN_MAX_LIN];   /* AGN_RELU_MASK of hidden layer l < nlin-1 (required for ReLU) */
+  int act_fn;                      /* AGN_ACT_* of the forward */
+  int _pad3;
+  const void* pre[AGN_MAX_LIN];    /* act_fn != ReLU: the forward's pre[l] (required), layout as act[l] */
 } agn_mlp_bwd_args;
 
 /* AGN_TILED layout of a [rows][H] activation saved for the backward (H = hidden, rows padded to
@@ -471,13 +480,19 @@ typedef struct {
   const double* add[2]; /* NULL or addends: add[q] + (add_idx[q] ? add_idx[q][r] : r) * add_ld[q] */
   const int32_t* add_idx[2];
   int add_ld[2];
-  const double* mask;   /* NULL, or out = 0 where mask <= 0 (ReLU backward on the saved activation) */
+  const double* mask;   /* NULL, or the activation backward: mask_act 0: out = 0 where mask <= 0
+                           (ReLU on the saved activation); 1 + AGN_ACT_*: out *= f'(mask), mask = the
+                           saved pre-activation */
   int mask_ld;
-  int relu;             /* out = max(out, 0) */
+  int relu;             /* 0: none; 1: out = max(out, 0); 1 + AGN_ACT_*: out = f(out) */
   double* out;
   int out_ld;
+  int mask_act;
+  double* pre_out;      /* NULL, or the value before the activation (relu > 1) is also written here */
+  int pre_ld;
+  int _pad3;
 } agn_f64_gemm_args;
-/* out = relu?(mask?(sum_seg A_seg B_seg + bias + add0 + add1)). Linear forward: transw = 1 (w = W
+/* out = f?(mask?(sum_seg A_seg B_seg + bias + add0 + add1)). Linear forward: transw = 1 (w = W
  * + column offset, ldw = in_features); input gradient: transw = 0. mlp.py:40-51, mgnLayer.py:97-103 */
 int agn_f64_gemm(const agn_f64_gemm_args* a, void* stream);
 typedef struct {

@@ -94,14 +94,14 @@ def edge_block_sum(p, pre, e, x, ei, n_hid):
 
 
 # models/mgnLayer.py:32-49 (EdgeBlock.forward, do_concat_trick=False)
-def edge_block_cat(p, pre, e, x, ei, n_hid):
+def edge_block_cat(p, pre, e, x, ei, n_hid, act=F.relu):
     row, col = ei
     h = torch.cat([e, x[row], x[col]], dim=-1)
-    return mlp(p, f"{pre}.mlp", h, mlp_nlin(n_hid), ln=f"{pre}.mlp.layer_norm.weight" in p)
+    return mlp(p, f"{pre}.mlp", h, mlp_nlin(n_hid), ln=f"{pre}.mlp.layer_norm.weight" in p, act=act)
 
 
 # models/mgnLayer.py:134-153 (NodeBlock.forward)
-def node_block(p, pre, x, e, ei, n_hid, aggregation="add"):
+def node_block(p, pre, x, e, ei, n_hid, aggregation="add", act=F.relu):
     row, col = ei
     if aggregation == "mean":
         agg = scatter_mean(e, col, dim=0, dim_size=x.size(0))
@@ -110,7 +110,13 @@ def node_block(p, pre, x, e, ei, n_hid, aggregation="add"):
     else:
         raise ValueError(f"Unsupported aggregation method: {aggregation}")
     h = torch.cat([x, agg], dim=-1)
-    return mlp(p, f"{pre}.mlp", h, mlp_nlin(n_hid), ln=f"{pre}.mlp.layer_norm.weight" in p)
+    return mlp(p, f"{pre}.mlp", h, mlp_nlin(n_hid), ln=f"{pre}.mlp.layer_norm.weight" in p, act=act)
+
+
+# mlp.py:37: the MLPs' activation (getattr(F, activation_fn)); EdgeBlockSum's chain is always ReLU
+# (mgnLayer.py:81)
+def act_of(cfg):
+    return getattr(F, cfg.get("activation_fn", "relu"))
 
 
 # models/mgnLayer.py:177-213 (MeshGraphNetLayer.forward; memory-logging syncs omitted on CPU)
@@ -118,20 +124,21 @@ def gmp_layer(p, pre, x, e, ei, cfg):
     if cfg.get("do_concat_trick", False):
         e_new = edge_block_sum(p, f"{pre}.edge_block", e, x, ei, cfg["n_hid_edge"])
     else:
-        e_new = edge_block_cat(p, f"{pre}.edge_block", e, x, ei, cfg["n_hid_edge"])
+        e_new = edge_block_cat(p, f"{pre}.edge_block", e, x, ei, cfg["n_hid_edge"], act=act_of(cfg))
     e = e + e_new
-    x_new = node_block(p, f"{pre}.node_block", x, e, ei, cfg["n_hid_node"], cfg.get("aggregation", "add"))
+    x_new = node_block(p, f"{pre}.node_block", x, e, ei, cfg["n_hid_node"], cfg.get("aggregation", "add"),
+                       act=act_of(cfg))
     x = x + x_new
     return x, e
 
 
 # models/mgn.py:108-139
 def mgn_forward(p, x, ea, ei, cfg):
-    xh = mlp(p, "node_encoder", x, mlp_nlin(cfg["n_hid_node_enc"]))
-    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]))
+    xh = mlp(p, "node_encoder", x, mlp_nlin(cfg["n_hid_node_enc"]), act=act_of(cfg))
+    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]), act=act_of(cfg))
     for l in range(cfg["processor_size"]):
         xh, eh = gmp_layer(p, f"layers.{l}", xh, eh, ei, cfg)
-    return mlp(p, "decoder", xh, mlp_nlin(cfg["n_hid_dec"]), ln=False)
+    return mlp(p, "decoder", xh, mlp_nlin(cfg["n_hid_dec"]), ln=False, act=act_of(cfg))
 
 
 # models/bsms_mgn.py:217-301 (_downsample). `stable` selects the build's documented tie rule
@@ -187,8 +194,8 @@ def bsms_schedule(processor_size, num_scales, layers_per_scale):
 def bsms_forward(p, x, ea, ei, cfg, batch=None, pos=None, stable=False):
     if batch is None:
         batch = x.new_zeros(x.size(0), dtype=torch.long)
-    nh = mlp(p, "node_encoder", x, mlp_nlin(cfg["n_hid_node_enc"]))
-    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]))
+    nh = mlp(p, "node_encoder", x, mlp_nlin(cfg["n_hid_node_enc"]), act=act_of(cfg))
+    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]), act=act_of(cfg))
     down, bott, up = bsms_schedule(cfg["processor_size"], cfg["num_scales"], cfg["layers_per_scale"])
     assigns, skips = [], []
     cb, cp, cei, ce, cn = batch, pos, ei, eh, nh
@@ -209,7 +216,7 @@ def bsms_forward(p, x, ea, ei, cfg, batch=None, pos=None, stable=False):
             ce, cei, cb, cp = se, sei, sb, sp
         for l in range(cnt):
             cn, ce = gmp_layer(p, f"up_layers.{s}.{l}", cn, ce, cei, cfg)
-    return mlp(p, "decoder", cn, mlp_nlin(cfg["n_hid_dec"]), ln=False)
+    return mlp(p, "decoder", cn, mlp_nlin(cfg["n_hid_dec"]), ln=False, act=act_of(cfg))
 
 
 # torch_geometric.nn.global_{add,mean,max}_pool (PyG; unpinned, not installed): size = batch.max()+1,
@@ -229,18 +236,18 @@ def global_pool(x, batch, method):
 
 # models/poolmgn.py:120-158 (poolMGN.forward)
 def poolmgn_forward(p, x, ea, ei, cfg, batch=None):
-    g = mlp(p, "global_encoder", x, mlp_nlin(cfg["n_hid_global_enc"]), ln=False)
+    g = mlp(p, "global_encoder", x, mlp_nlin(cfg["n_hid_global_enc"]), ln=False, act=act_of(cfg))
     if batch is not None:
         g = global_pool(g, batch, cfg["global_pool_method"])
         g = g.repeat_interleave(torch.bincount(batch), dim=0)
     else:
         g = global_pool(g, torch.zeros(x.size(0), dtype=torch.long), cfg["global_pool_method"])
         g = g.repeat(x.size(0), 1)
-    xh = mlp(p, "node_encoder", torch.cat((x, g), dim=-1), mlp_nlin(cfg["n_hid_node_enc"]))
-    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]))
+    xh = mlp(p, "node_encoder", torch.cat((x, g), dim=-1), mlp_nlin(cfg["n_hid_node_enc"]), act=act_of(cfg))
+    eh = mlp(p, "edge_encoder", ea, mlp_nlin(cfg["n_hid_edge_enc"]), act=act_of(cfg))
     for l in range(cfg["processor_size"]):
         xh, eh = gmp_layer(p, f"layers.{l}", xh, eh, ei, cfg)
-    return mlp(p, "decoder", xh, mlp_nlin(cfg["n_hid_dec"]), ln=False)
+    return mlp(p, "decoder", xh, mlp_nlin(cfg["n_hid_dec"]), ln=False, act=act_of(cfg))
 
 
 def cfg_from_kwargs(**kw):
@@ -259,6 +266,7 @@ def cfg_from_kwargs(**kw):
         stride=kw.get("stride", 2),
         global_pool_method=kw.get("global_pool_method", "mean"),
         n_hid_global_enc=kw.get("num_hidden_layers_global_encoder", 1),
+        activation_fn=kw.get("activation_fn", "relu"),
     )
 
 

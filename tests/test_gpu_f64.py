@@ -27,18 +27,20 @@ def _check(name, got, ref, tol=TOL):
     assert r <= tol, (name, r)
 
 
-@pytest.mark.parametrize("n_hid,in_dim,out_dim,ln", [(2, 10, 64, True), (0, 7, 4, False), (1, 128, 128, True)])
-def test_f64_mlp_vs_oracle(n_hid, in_dim, out_dim, ln):
+@pytest.mark.parametrize("n_hid,in_dim,out_dim,ln,act", [(2, 10, 64, True, "relu"), (0, 7, 4, False, "relu"),
+                                                         (1, 128, 128, True, "relu"), (2, 10, 64, True, "gelu"),
+                                                         (2, 10, 64, True, "silu"), (2, 10, 64, True, "tanh")])
+def test_f64_mlp_vs_oracle(n_hid, in_dim, out_dim, ln, act):
     from models.mlp import MLP
     from oracle import refcpu as R
     torch.manual_seed(0)
-    m = MLP(in_dim, 128, out_dim, num_hidden_layers=n_hid, use_layer_norm=ln).double()
+    m = MLP(in_dim, 128, out_dim, num_hidden_layers=n_hid, activation_fn=act, use_layer_norm=ln).double()
     g = torch.Generator().manual_seed(1)
     x = torch.randn(3001, in_dim, generator=g, dtype=torch.float64)
     gy = torch.randn(3001, out_dim, generator=g, dtype=torch.float64)
     p = {f"m.{k}": v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
     xr = x.clone().requires_grad_(True)
-    ref = R.mlp(p, "m", xr, R.mlp_nlin(n_hid), ln=ln)
+    ref = R.mlp(p, "m", xr, R.mlp_nlin(n_hid), ln=ln, act=R.act_of({"activation_fn": act}))
     ref.backward(gy)
     m = m.to(DEV)
     xg = x.to(DEV).requires_grad_(True)
@@ -83,6 +85,29 @@ def test_f64_gmp_layer_fwd_bwd_vs_oracle(trick, aggregation):
     _check("de", eg.grad, er.grad)
     for n, q in layer.named_parameters():
         _check(f"d{n}", q.grad, p[f"L.{n}"].grad)
+
+
+def test_f64_layer_gelu_golden():
+    """The reference's float64 MeshGraphNetLayer with activation_fn='gelu' (tests/golden, made by
+    tools/make_goldens.py from the reference itself): the node chain on GELU, the sum-trick edge
+    chain on ReLU (mgnLayer.py:81)."""
+    from golden_util import load, params
+    from models.mgnLayer import MeshGraphNetLayer
+    d, m = load("layer_sum_h32_f64_gelu")
+    H, nh = m["H"], m["n_hid"]
+    layer = MeshGraphNetLayer(H, H, H, nh, nh, "gelu", True, m["aggregation"], m["trick"]).double()
+    layer.load_state_dict(params(d))
+    layer = layer.to(DEV)
+    x = d["x"].to(DEV).requires_grad_(True)
+    e = d["e"].to(DEV).requires_grad_(True)
+    xo, eo = layer(x, e, d["edge_index"].to(DEV))
+    torch.autograd.backward([xo, eo], [d["gx_out"].to(DEV), d["ge_out"].to(DEV)])
+    _check("x'", xo, d["x_out"])
+    _check("e'", eo, d["e_out"])
+    _check("dx", x.grad, d["gx"])
+    _check("de", e.grad, d["ge"])
+    for n, q in layer.named_parameters():
+        _check(f"d{n}", q.grad, d["gp:" + n])
 
 
 @pytest.mark.parametrize("kind", ["mgn", "bsms"])

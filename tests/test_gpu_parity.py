@@ -54,18 +54,37 @@ def _check_param_grads(model, d, tol=GPAR):
 
 
 # ------------------------------------------------------------------------------ MLP
-@pytest.mark.parametrize("name", ["mlp_nh0", "mlp_nh1", "mlp_nh2", "mlp_dec"])
+@pytest.mark.parametrize("name", ["mlp_nh0", "mlp_nh1", "mlp_nh2", "mlp_dec", "mlp_gelu_h128", "mlp_silu_h128",
+                                  "mlp_tanh_h128"])
 def test_mlp(name):
+    """MLP (mlp.py:40-51), including activation_fn gelu / silu / tanh (mlp.py:37) at H = 128."""
     from models.mlp import MLP
     d, m = load(name)
     model = _load(MLP(m["input_dim"], m["hidden_dim"], m["output_dim"], m["num_hidden_layers"],
-                      use_layer_norm=m["use_layer_norm"]), d)
+                      activation_fn=m.get("activation_fn", "relu"), use_layer_norm=m["use_layer_norm"]), d)
     x = d["x"].to(DEV).requires_grad_(True)
     y = model(x)
     _fwd_ok(y, d["y"])
     y.backward(d["gy"].to(DEV))
     assert rel_l2(x.grad.cpu(), d["gx"]) <= GIN
     _check_param_grads(model, d)
+
+
+@pytest.mark.parametrize("act", ["gelu", "silu", "tanh"])
+def test_mlp_activation_bf16(act):
+    """bf16 parameters and activations (train.py:30-34) with a non-ReLU activation_fn, against the
+    reference's fp32 fixture: SURVEY §8's bf16 bar (rel-L2 <= 2e-2) on y, dx and every weight grad."""
+    from models.mlp import MLP
+    d, m = load(f"mlp_{act}_h128")
+    model = _load(MLP(m["input_dim"], m["hidden_dim"], m["output_dim"], m["num_hidden_layers"],
+                      activation_fn=act, use_layer_norm=m["use_layer_norm"]), d).to(torch.bfloat16)
+    x = d["x"].to(DEV, torch.bfloat16).requires_grad_(True)
+    y = model(x)
+    y.backward(d["gy"].to(DEV, torch.bfloat16))
+    worst = max([rel_l2(y.float().cpu(), d["y"]), rel_l2(x.grad.float().cpu(), d["gx"])] +
+                [rel_l2(q.grad.float().cpu(), d["gp:" + n]) for n, q in model.named_parameters()])
+    print(f"bf16 MLP {act}: worst rel-L2 {worst:.2e} against the fp32 reference")
+    assert worst <= 2e-2
 
 
 # ------------------------------------------------------------------------------ blocks
@@ -94,7 +113,7 @@ def test_blocks(name):
 
 # ------------------------------------------------------------------------------ layers
 LAYERS = ["layer_sum_h32", "layer_sum_h32_shuf", "layer_cat_h32", "layer_mean_h32", "layer_sum_h128",
-          "layer_sum_h32_nh1"]
+          "layer_sum_h32_nh1", "layer_cat_h128_gelu", "layer_sum_h32_silu", "layer_cat_h32_tanh"]
 
 
 @pytest.mark.parametrize("name", LAYERS)
@@ -102,7 +121,8 @@ def test_layer(name):
     from models.mgnLayer import MeshGraphNetLayer
     d, m = load(name)
     H, nh = m["H"], m["n_hid"]
-    layer = _load(MeshGraphNetLayer(H, H, H, nh, nh, "relu", True, m["aggregation"], m["trick"]), d)
+    layer = _load(MeshGraphNetLayer(H, H, H, nh, nh, m.get("activation_fn", "relu"), True, m["aggregation"],
+                                    m["trick"]), d)
     x = d["x"].to(DEV).requires_grad_(True)
     e = d["e"].to(DEV).requires_grad_(True)
     xo, eo = layer(x, e, d["edge_index"].to(DEV))

@@ -27,7 +27,8 @@ def _check_grads(p, d, tol=GRAD_TOL):
         assert rel_l2(v.grad, g) <= tol, (k, rel_l2(v.grad, g))
 
 
-@pytest.mark.parametrize("name", ["mlp_nh0", "mlp_nh1", "mlp_nh2", "mlp_dec"])
+@pytest.mark.parametrize("name", ["mlp_nh0", "mlp_nh1", "mlp_nh2", "mlp_dec", "mlp_gelu_h128", "mlp_silu_h128",
+                                  "mlp_tanh_h128"])
 def test_mlp(name):
     d, m = load(name)
     p = _leaf(params(d))
@@ -35,7 +36,7 @@ def test_mlp(name):
     nlin = R.mlp_nlin(m["num_hidden_layers"])
     # MLP state dict keys have no module prefix: "layers.0.weight"
     pp = {"m." + k: v for k, v in p.items()}
-    y = R.mlp(pp, "m", x, nlin, ln=m["use_layer_norm"])
+    y = R.mlp(pp, "m", x, nlin, ln=m["use_layer_norm"], act=R.act_of(m))
     assert torch.equal(y, d["y"]) or rel_l2(y, d["y"]) <= FWD_TOL
     y.backward(d["gy"])
     assert rel_l2(x.grad, d["gx"]) <= GRAD_TOL
@@ -64,7 +65,8 @@ def test_blocks(name, kind):
 
 
 LAYERS = ["layer_sum_h32", "layer_sum_h32_shuf", "layer_cat_h32", "layer_mean_h32",
-          "layer_sum_h128", "layer_sum_h32_nh1", "layer_sum_h32_f64"]
+          "layer_sum_h128", "layer_sum_h32_nh1", "layer_sum_h32_f64",
+          "layer_cat_h128_gelu", "layer_sum_h32_silu", "layer_cat_h32_tanh", "layer_sum_h32_f64_gelu"]
 
 
 @pytest.mark.parametrize("name", LAYERS)
@@ -74,7 +76,7 @@ def test_layer(name):
     x = d["x"].clone().requires_grad_(True)
     e = d["e"].clone().requires_grad_(True)
     cfg = dict(do_concat_trick=m["trick"], n_hid_edge=m["n_hid"], n_hid_node=m["n_hid"],
-               aggregation=m["aggregation"])
+               aggregation=m["aggregation"], activation_fn=m.get("activation_fn", "relu"))
     xo, eo = R.gmp_layer(p, "L", x, e, d["edge_index"], cfg)
     assert torch.equal(xo, d["x_out"]) or rel_l2(xo, d["x_out"]) <= FWD_TOL
     assert torch.equal(eo, d["e_out"]) or rel_l2(eo, d["e_out"]) <= FWD_TOL

@@ -161,11 +161,11 @@ def case_mlp():
                          use_layer_norm=False), x=x, y=y, gy=gy, gx=x.grad, **sd(m), **grads(m))
 
 
-def case_layer(name, H, nu, nv, trick, agg="add", nh=2, shuffle=False, dtype=torch.float32):
+def case_layer(name, H, nu, nv, trick, agg="add", nh=2, shuffle=False, dtype=torch.float32, act="relu"):
     torch.manual_seed(1)
     t = mesh_tensors(nu, nv, shuffle=shuffle)
     N, E = t["x"].shape[0], t["edge_index"].shape[1]
-    layer = MeshGraphNetLayer(H, H, H, nh, nh, "relu", True, agg, trick).to(dtype)
+    layer = MeshGraphNetLayer(H, H, H, nh, nh, act, True, agg, trick).to(dtype)
     x = torch.randn(N, H, dtype=dtype, requires_grad=True)
     e = torch.randn(E, H, dtype=dtype, requires_grad=True)
     ei = t["edge_index"]
@@ -173,9 +173,29 @@ def case_layer(name, H, nu, nv, trick, agg="add", nh=2, shuffle=False, dtype=tor
     gx = torch.randn_like(xo)
     ge = torch.randn_like(eo)
     torch.autograd.backward([xo, eo], [gx, ge])
-    meta = dict(H=H, trick=trick, aggregation=agg, n_hid=nh, dtype=str(dtype))
+    meta = dict(H=H, trick=trick, aggregation=agg, n_hid=nh, dtype=str(dtype), activation_fn=act)
     save(name, meta, x=x, e=e, edge_index=ei, x_out=xo, e_out=eo, gx_out=gx, ge_out=ge,
          gx=x.grad, ge=e.grad, **sd(layer), **grads(layer))
+
+
+def case_act():
+    """activation_fn gelu / silu / tanh (mlp.py:37 getattr(F, activation_fn)): an MLP per activation
+    at H = 128; concat-EdgeBlock layers (both chains take the activation) and a sum-trick layer (its
+    edge chain stays ReLU, mgnLayer.py:81; the node chain takes it); a float64 layer with GELU."""
+    for act in ("gelu", "silu", "tanh"):
+        torch.manual_seed(9)
+        m = MLP(6, 128, 128, num_hidden_layers=2, activation_fn=act)
+        x = torch.randn(70, 6, requires_grad=True)
+        y = m(x)
+        gy = torch.randn_like(y)
+        y.backward(gy)
+        save(f"mlp_{act}_h128", dict(input_dim=6, hidden_dim=128, output_dim=128, num_hidden_layers=2,
+                                     use_layer_norm=True, activation_fn=act),
+             x=x, y=y, gy=gy, gx=x.grad, **sd(m), **grads(m))
+    case_layer("layer_cat_h128_gelu", 128, 8, 6, False, shuffle=True, act="gelu")
+    case_layer("layer_sum_h32_silu", 32, 10, 6, True, act="silu")
+    case_layer("layer_cat_h32_tanh", 32, 10, 6, False, shuffle=True, act="tanh")
+    case_layer("layer_sum_h32_f64_gelu", 32, 10, 6, True, dtype=torch.float64, act="gelu")
 
 
 def case_blocks():
@@ -358,3 +378,4 @@ if __name__ == "__main__":
     case_downsample()
     case_bf16()
     case_fp16()
+    case_act()
