@@ -613,28 +613,27 @@ constexpr int ROUND_ROWS = CW * 32;
 struct DpdWalk {
   int cur;    // receiver of the open run (-1 at a round's start: the round's first row opens one)
   float sum;  // its fp32 sum (lanes 0-31: feature 32d + lane)
-  int dvn;    // receivers of the next L1 pair's tile (lanes 0-31), loaded a pair ahead
 #ifdef AGN_EB_STAMPS
   unsigned long long t_mm = 0, t_walk = 0;  // cycles in the G0 recompute (to the release) / the walk
 #endif
 };
 
-// receivers of a tile's rows (lane c & 31: row 32 tile + c, clamped to the last row)
-AGN_DEV int dpd_ids(const agn_edge_bwd_args& a, int tile, int lane) {
-  return a.dst[min(tile * 32 + (lane & 31), a.rows - 1)];
-}
+// The receiver ids are read with scalar loads (constant address space: s_load, counted by lgkmcnt).
+// A vector load would be waited for with vmcnt, which also counts the walk's own dP_d stores: every
+// walk would then wait for the previous walk's 32 stores to be acknowledged.
+typedef __attribute__((address_space(4))) const int32_t cint32;
 
-// one row of the walk: restart the sum at a new receiver, add the row, store the running sum.
-// A raw buffer store: the descriptor (dpd_rsrc) spans the 64-byte slice dP_d[0][32d..32d+31], the
-// row is the SGPR offset n * 256 (outside the range check, which covers the VGPR offset only), and
-// lanes 32-63 address past the slice's end and are dropped, so the store needs no exec-mask branch.
-AGN_DEV __amdgpu_buffer_rsrc_t dpd_rsrc(const agn_edge_bwd_args& a, int d) {
-  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<bf16*>(a.dpd) + 32 * d, 0, 64, 0x00020000);
-}
-AGN_DEV void dpd_row(DpdWalk& st, int n, float v, __amdgpu_buffer_rsrc_t rs, int voff) {
+// one row of the walk: restart the sum at a new receiver, add the row, store the running sum
+// (lanes 0-31: a uniform row base and a 32-bit lane offset)
+AGN_DEV void dpd_row(const agn_edge_bwd_args& a, DpdWalk& st, int n, float v, int d, int lane) {
   st.sum = (n != st.cur ? 0.f : st.sum) + v;
   st.cur = n;
-  __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(short, (bf16)st.sum), rs, voff, n * (H * 2), 0);
+#ifdef AGN_EB_DPD_NOSTORE  // diagnostic build only (the walk's cost without its stores; dP_d is wrong)
+  if (st.sum == 12345.678f) lane = 0;  // keeps the sum live
+  else return;
+#endif
+  bf16* rowp = reinterpret_cast<bf16*>(a.dpd) + ((size_t)n * H + 32 * d);
+  if (lane < 32) rowp[lane] = (bf16)st.sum;
 }
 
 // dP_d of a tile's L1 pair (ring slots k0, k1), then release() the slots. The ring reads stream
@@ -642,13 +641,28 @@ AGN_DEV void dpd_row(DpdWalk& st, int n, float v, __amdgpu_buffer_rsrc_t rs, int
 // the pair's 40 registers of G1 / a1 across a release) and the slots are released after the
 // last MFMA, before the row walk.
 template <typename Release>
-AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k1, int tile, int next_tile, int d,
-                      int lane, DpdWalk& st, Release release) {
+AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k1, int tile, int d, int lane,
+                      DpdWalk& st, Release release) {
 #ifdef AGN_EB_STAMPS
   const unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #endif
   lane = fresh_lane(lane);  // lane-derived offsets are formed here, not hoisted out of the dW loop
   const int c = lane & 31, hh = lane >> 5;
+  // the tile's 32 receivers: contiguous scalar loads (two s_load_dwordx16), their latency under the
+  // MFMAs below. The last tile of the edge list, if partial, reads them with a vector load (clamped
+  // rows) and pays its wait once.
+  const int row0 = tile * 32;
+  const int nval = min(32, a.rows - row0);
+  const bool full = nval == 32;
+  int ids[32];
+  int dvec = 0;
+  if (full) {
+    cint32* dsc = (cint32*)(a.dst) + row0;  // (a C-style cast: the address-space conversion)
+#pragma unroll
+    for (int r = 0; r < 32; ++r) ids[r] = dsc[r];
+  } else {
+    dvec = a.dst[min(row0 + c, a.rows - 1)];
+  }
   const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
   // [a1 > 0] at D's places, as 16 bits: transposed reads of the items' a1 images. Register 4m + j
   // of lane (c, hh) is row 8m + 4hh + j, feature 32d + c; lane 4j + p of each 16-lane group
@@ -711,13 +725,6 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
     gv[k] = (keep >> k) & 1 ? lo_bf16(pk) : 0.f;
     gv[k + 1] = (keep >> (k + 1)) & 1 ? hi_bf16(pk) : 0.f;
   }
-  // the receivers, waited for once (an opaque copy: no per-row waits behind the walk's stores)
-  int dvw = st.dvn;
-  opaque(dvw);
-  if (next_tile >= 0) st.dvn = dpd_ids(a, next_tile, lane);
-  const int nval = min(32, a.rows - tile * 32);
-  const int voff = hh ? 64 : 2 * c;  // dpd_row's store offset (lanes 32-63: dropped)
-  const __amdgpu_buffer_rsrc_t rs = dpd_rsrc(a, d);
   // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
   // lanes 0-31 take over by v_permlane32_swap, four registers at a time. Full tiles walk
   // straight-line code; only the last tile of the edge list checks its row count.
@@ -730,13 +737,13 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
       v[4 + j] = __uint_as_float(
           __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[4 * m + j]), __float_as_uint(gv[4 * m + j]), false, false)[1]);
     }
-    if (nval == 32) {
+    if (full) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dpd_row(st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], rs, voff);
+      for (int j = 0; j < 8; ++j) dpd_row(a, st, ids[8 * m + j], v[j], d, lane);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        if (8 * m + j < nval) dpd_row(st, __builtin_amdgcn_readlane(dvw, 8 * m + j), v[j], rs, voff);
+        if (8 * m + j < nval) dpd_row(a, st, __builtin_amdgcn_readlane(dvec, 8 * m + j), v[j], d, lane);
     }
     sched_fence();
   }
@@ -820,8 +827,7 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   unsigned long long waited = 0;
   const unsigned long long tstart = __builtin_amdgcn_s_memtime();
 #endif
-  DpdWalk dw_run{-1, 0.f, 0};
-  if (a.dpd && rw.first < rw.end) dw_run.dvn = dpd_ids(a, rw.first * CW, lane);
+  DpdWalk dw_run{-1, 0.f};
   for (int rd = rw.first; rd < rw.end; rd += rw.step) {
     const int cmax = min(CW, ntiles - rd * CW);
     dw_run.cur = -1;  // a round's first row opens a run (one that began earlier is dpd_cross_kernel's)
@@ -890,9 +896,7 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
         }
         if (dp) {
           sched_fence();  // the dW MFMAs have taken gf / xf before these reads claim registers
-          const int t = grp * GROUP + cc;  // the L1 pairs come in tile order
-          const int nxt = t + 1 < cmax ? rd * CW + t + 1 : (rd + rw.step < rw.end ? (rd + rw.step) * CW : -1);
-          dpd_pair(a, lds, k0, k1, rd * CW + t, nxt, d, lane, dw_run, release);
+          dpd_pair(a, lds, k0, k1, rd * CW + grp * GROUP + cc, d, lane, dw_run, release);  // (L1 pairs: tile order)
         }
       }
     }
@@ -1016,8 +1020,7 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;
-  // dpd_row's SGPR row offset n * 256 is 32-bit: nodes < 2^24
-  if (a->dpd && (!a->rowptr || a->nodes < 1 || a->nodes >= (1 << 24) || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
+  if (a->dpd && (!a->rowptr || a->nodes < 1 || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
                  (reinterpret_cast<uintptr_t>(a->g0) & 15)))
     return AGN_E_ARG;
   hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
