@@ -28,10 +28,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #define AGN_DEV __device__ __forceinline__
 
-// A/B switch: the edge forwards' e' stores as non-temporal stores
-#ifndef AGN_NT_STORE
-#define AGN_NT_STORE 0
-#endif
 namespace agn {
 
 enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
@@ -351,13 +347,7 @@ struct PendingRow {
   AGN_DEV void flush(int h) {
     if (p && valid) {
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-#if AGN_NT_STORE
-        __builtin_nontemporal_store(d[i], reinterpret_cast<u32x4*>(p + 16 * i + 8 * h));
-#else
-        *reinterpret_cast<u32x4*>(p + 16 * i + 8 * h) = d[i];
-#endif
-      }
+      for (int i = 0; i < N; ++i) *reinterpret_cast<u32x4*>(p + 16 * i + 8 * h) = d[i];
     }
     p = nullptr;
   }

@@ -196,13 +196,7 @@ AGN_DEV void store_raw(bf16* rowp, const uint4 (&o)[4], int lane, bool valid) {
   const int g = lane >> 4;
   if (valid) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-#if AGN_NT_STORE
-      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o[t]), reinterpret_cast<u32x4*>(rowp + 32 * t + 8 * g));
-#else
-      *reinterpret_cast<uint4*>(rowp + 32 * t + 8 * g) = o[t];
-#endif
-    }
+    for (int t = 0; t < 4; ++t) *reinterpret_cast<uint4*>(rowp + 32 * t + 8 * g) = o[t];
   }
 }
 AGN_DEV void store_op(bf16* rowp, const Op& o, int lane, bool valid) {

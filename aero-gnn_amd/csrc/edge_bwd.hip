@@ -623,15 +623,11 @@ struct DpdWalk {
 // walk would then wait for the previous walk's 32 stores to be acknowledged.
 typedef __attribute__((address_space(4))) const int32_t cint32;
 
-// one row of the walk: restart the sum at a new receiver, add the row, store the running sum
-// (lanes 0-31: a uniform row base and a 32-bit lane offset)
+// one row of the sequential walk (the last, partial tile of an edge list): restart the sum at a new
+// receiver, add the row, store the running sum (lanes 0-31: a uniform row base, 32-bit lane offset)
 AGN_DEV void dpd_row(const agn_edge_bwd_args& a, DpdWalk& st, int n, float v, int d, int lane) {
   st.sum = (n != st.cur ? 0.f : st.sum) + v;
   st.cur = n;
-#ifdef AGN_EB_DPD_NOSTORE  // diagnostic build only (the walk's cost without its stores; dP_d is wrong)
-  if (st.sum == 12345.678f) lane = 0;  // keeps the sum live
-  else return;
-#endif
   bf16* rowp = reinterpret_cast<bf16*>(a.dpd) + ((size_t)n * H + 32 * d);
   if (lane < 32) rowp[lane] = (bf16)st.sum;
 }
@@ -717,6 +713,9 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
   const unsigned long long c1 = __builtin_amdgcn_s_memtime();
   st.t_mm += c1 - c0;
 #endif
+  // The walk below is VALU work that holds up nothing: it runs at the chain wave's priority, so it
+  // takes the SIMD's issue cycles the (issue-bound) chain wave leaves idle instead of preempting it
+  __builtin_amdgcn_s_setprio(0);
   // G0 = round(D) where a1 > 0
   float gv[16];
 #pragma unroll
@@ -725,28 +724,71 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
     gv[k] = (keep >> k) & 1 ? lo_bf16(pk) : 0.f;
     gv[k + 1] = (keep >> (k + 1)) & 1 ? hi_bf16(pk) : 0.f;
   }
-  // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
-  // lanes 0-31 take over by v_permlane32_swap, four registers at a time. Full tiles walk
-  // straight-line code; only the last tile of the edge list checks its row count.
+  if (full) {
+    // Two halves in lockstep. swap(a, b) = (a.lo | b.lo, a.hi | b.hi) of v_permlane32_swap puts
+    // rows 0-15 in lanes 0-31 and rows 16-31 in lanes 32-63, same features: local row r = 8m + j
+    // of either half is A[4m + j] (j < 4) or B[4m + j - 4] (j >= 4).
+    float A[8], B[8];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = gv[4 * m + j];
-      v[4 + j] = __uint_as_float(
-          __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[4 * m + j]), __float_as_uint(gv[4 * m + j]), false, false)[1]);
+    for (int k = 0; k < 8; ++k) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[k]), __float_as_uint(gv[k + 8]), false, false);
+      A[k] = __uint_as_float(sw[0]);
+      B[k] = __uint_as_float(sw[1]);
     }
-    if (full) {
+    auto row_v = [&](int r) { return (r & 7) < 4 ? A[4 * (r >> 3) + (r & 7)] : B[4 * (r >> 3) + (r & 7) - 4]; };
+    // byte offset of (receiver n, this lane's feature) in dP_d: 32-bit (nodes < 2^24), so the store
+    // takes the scalar base + vector offset form
+    const uint32_t voff = 64 * d + 2 * c;
+    char* const dpb = reinterpret_cast<char*>(a.dpd);
+    auto put = [&](int n, float v) { *reinterpret_cast<bf16*>(dpb + ((uint32_t)n * (H * 2) + voff)) = (bf16)v; };
+    // the open run per lane: lanes 0-31 carry it from the previous tile, lanes 32-63 open one at row 16
+    int cur = hh ? -1 : st.cur;
+    float sum = st.sum;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dpd_row(a, st, ids[8 * m + j], v[j], d, lane);
-    } else {
+    for (int r = 0; r < 16; ++r) {
+      const int n = hh ? ids[16 + r] : ids[r];
+      sum = (n != cur ? 0.f : sum) + row_v(r);
+      cur = n;
+      put(n, sum);
+    }
+    // Rows 15 and 16 of one receiver: the upper half summed that run from zero above. Redo it from
+    // the lower half's sum, in row order (these stores land after the walk's, so they stand).
+    if (ids[16] == ids[15]) {
+      float s2 = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false)[0]);
+      bool through = true;  // the run covers rows 16-31: it is the tile's open run
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (ids[16 + r] != ids[15]) {
+          through = false;
+          break;
+        }
+        s2 += row_v(r);
+        if (hh) put(ids[15], s2);
+      }
+      if (through) sum = s2;
+    }
+    // the tile's open run (row 31's receiver) goes to the next tile in lanes 0-31
+    st.sum = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false)[1]);
+    st.cur = ids[31];
+  } else {
+    // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
+    // lanes 0-31 take over by v_permlane32_swap, four registers at a time
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = gv[4 * m + j];
+        v[4 + j] = __uint_as_float(
+            __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[4 * m + j]), __float_as_uint(gv[4 * m + j]), false, false)[1]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (8 * m + j < nval) dpd_row(a, st, __builtin_amdgcn_readlane(dvec, 8 * m + j), v[j], d, lane);
+      sched_fence();
     }
-    sched_fence();
   }
+  __builtin_amdgcn_s_setprio(2);
 #ifdef AGN_EB_STAMPS
   st.t_walk += __builtin_amdgcn_s_memtime() - c1;
 #endif
@@ -1020,7 +1062,8 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;
-  if (a->dpd && (!a->rowptr || a->nodes < 1 || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
+  // (the dP_d walk addresses rows with 32-bit byte offsets: nodes < 2^24)
+  if (a->dpd && (!a->rowptr || a->nodes < 1 || a->nodes >= (1 << 24) || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
                  (reinterpret_cast<uintptr_t>(a->g0) & 15)))
     return AGN_E_ARG;
   hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);

@@ -389,7 +389,7 @@ typedef struct {
    * receivers whose edges span a round boundary, and zeroes the empty ones. */
   void* dpd;                 /* [nodes][128] out, or NULL */
   const int32_t* rowptr;     /* [nodes + 1] receiver offsets of dst (dst sorted: CSC order) */
-  int nodes;
+  int nodes;                 /* < 2^24 */
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
