@@ -18,6 +18,7 @@ MAX_SEG = 3
 F32, BF16, F16, F64 = 0, 1, 2, 3
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
 OPT_RESIDENT = 0
+OPT_EDGE_FWD_HALVES = 1
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -249,6 +250,10 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = _Lib(L)
+        # A/B measurements: agn_edge_forward's halves per wave (AGN_OPT_EDGE_FWD_HALVES)
+        nh = os.environ.get("AEROGNN_EDGE_FWD_HALVES")
+        if nh and L.agn_set_option(OPT_EDGE_FWD_HALVES, int(nh)) < 0:
+            raise AeroGNNError(f"AEROGNN_EDGE_FWD_HALVES={nh}: 1 or 2")
     return _lib
 
 

@@ -114,6 +114,34 @@ AGN_DEV void gemm_fwd(f32x4 (&acc)[8], const Op& x, const char* lds, int img_off
   }
 }
 
+// gemm_fwd for NH 16-row halves of a wave at once: each weight fragment read from LDS feeds NH
+// MFMAs (one per half), so the LDS traffic per row falls by NH. Every accumulator sums its k-steps
+// in gemm_fwd's order: the results are bitwise gemm_fwd's.
+template <int NH>
+AGN_DEV void gemm_fwd_n(f32x4 (&acc)[NH][8], const Op (&x)[NH], const char* lds, int img_off, int lane) {
+  const char* img = lds + sfresh(img_off);
+  const int m = lane & 15, g = lane >> 4;
+  const int base = wimg(8 * (m >> 2) + (m & 3), g, 0);
+  auto frag = [&](int idx) {
+    const int t = idx >> 3, ob = idx & 7;
+    const int ro = 256 * (32 * (ob >> 1) + 4 * (ob & 1));
+    const uint2 lo = *reinterpret_cast<const uint2*>(img + (base ^ (64 * t)) + ro);
+    const uint2 hi = *reinterpret_cast<const uint2*>(img + (base ^ (64 * t) ^ 8) + ro);
+    return frag2(lo, hi);
+  };
+  bf16x8 f[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) f[i] = frag(i);
+#pragma unroll
+  for (int idx = 0; idx < 32; ++idx) {
+    const bf16x8 cur = f[idx % PF];
+    if (idx + PF < 32) f[idx % PF] = frag(idx + PF);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) acc[h][idx & 7] = mfma16(cur, x[h].u[idx >> 3], acc[h][idx & 7]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // acc[ib] = W^T[rows of block ib] . G^T (from zero; t ascending). A[m][k = 8g + j] =
 // W[32t + 8g + j][in(ib, m)]: per 16-lane group g, lane 4q + p supplies row 32t + 8g + q (+4 for
 // j >= 4) at the 4 columns in(ib, 4p..4p+3) = 32(ib>>1) + 8p + 4(ib&1) + 0..3 (chunk 4(ib>>1) + p,

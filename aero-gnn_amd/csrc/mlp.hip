@@ -1279,11 +1279,16 @@ extern "C" int agn_debug_fwd_stamps(void* p) {
 }
 #endif
 
+namespace agn {
+int edge16_fwd_set_halves(int nh);  // edge16_fwd.hip
+}
+
 extern "C" {
 
 int agn_version(void) { return 1; }
 
 int agn_set_option(int key, int value) {
+  if (key == AGN_OPT_EDGE_FWD_HALVES) return agn::edge16_fwd_set_halves(value);
   if (key == AGN_OPT_RESIDENT) {
     const int old = g_opt_resident;
     g_opt_resident = value ? 1 : 0;

@@ -196,8 +196,10 @@ int agn_version(void);
 const char* agn_error_string(int code);
 /* Process-wide kernel-selection options (testing / A-B measurement). Returns the previous value
  * or AGN_E_ARG. AGN_OPT_RESIDENT: 1 (default) = persistent resident-weight kernels for the
- * large bf16 H=128 edge MLPs, 0 = always the general kernels (bitwise-identical outputs). */
-enum { AGN_OPT_RESIDENT = 0 };
+ * large bf16 H=128 edge MLPs, 0 = always the general kernels (bitwise-identical outputs).
+ * AGN_OPT_EDGE_FWD_HALVES: 16-row halves per wave of agn_edge_forward, 1 or 2 (default; bitwise-
+ * identical outputs; agn_edge_fwd_blocks follows it). */
+enum { AGN_OPT_RESIDENT = 0, AGN_OPT_EDGE_FWD_HALVES = 1 };
 int agn_set_option(int key, int value);
 /* bytes of a packed A operand with `m` rows and `k` reduction columns */
 size_t agn_packed_bytes(int m, int k, int dtype);

@@ -292,6 +292,31 @@ def test_edge16_backward_deterministic_and_close_to_round4_kernel():
         assert r <= 5e-2, (k, r)
 
 
+@pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (40000, 240000)])
+def test_edge16_forward_halves_bitwise(N, E):
+    """agn_edge_forward's two variants (one or two 16-row halves per wave, AGN_OPT_EDGE_FWD_HALVES)
+    give bitwise-equal outputs and saves: every accumulator sums the same products in the same order."""
+    from aerognn import _lib as L
+    ch = Chain(18)
+    src, dst = _level(N, E, 19)
+    e, P, _, _ = _inputs(N, E, 20)
+    lib = L.lib()
+    old = lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, 1)
+    try:
+        one = _forward(ch, e, P, src, dst)
+        lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, 2)
+        two = _forward(ch, e, P, src, dst)
+    finally:
+        lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, old)
+    torch.cuda.synchronize()
+    out1, acts1, hpre1, stats1 = one
+    out2, acts2, hpre2, stats2 = two
+    assert torch.equal(out1, out2)
+    for a1, a2 in zip(acts1, acts2):
+        assert torch.equal(a1, a2)
+    assert torch.equal(hpre1, hpre2) and torch.equal(stats1, stats2)
+
+
 def test_edge16_forward_close_to_round4_kernel():
     from aerognn import core
     from aerognn import _lib as L
