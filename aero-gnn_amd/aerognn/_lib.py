@@ -19,6 +19,9 @@ F32, BF16, F16, F64 = 0, 1, 2, 3
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
 OPT_RESIDENT = 0
 OPT_EDGE_FWD_HALVES = 1
+OPT_EDGE_FWD_WAVES = 2
+OPT_EDGE_FWD32_WAVES = 3
+OPT_EDGE_FWD32_PRIO = 4
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -130,7 +133,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
-            "agn_edge_forward", "agn_edge_backward",
+            "agn_edge_forward", "agn_edge_forward32", "agn_edge_backward",
             "agn_proj_forward", "agn_proj_backward")
 
 
@@ -230,6 +233,8 @@ def lib():
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_edge_fwd_blocks": (i32, [i32]),
             "agn_edge_forward": (i32, [C.POINTER(EdgeFwdArgs), vp]),
+            "agn_edge_fwd32_blocks": (i32, [i32]),
+            "agn_edge_forward32": (i32, [C.POINTER(EdgeFwdArgs), vp]),
             "agn_edge_backward_blocks": (i32, [i32]),
             "agn_edge_backward": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_fault_status": (i32, [C.POINTER(i32), i32]),
@@ -250,10 +255,15 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = _Lib(L)
-        # A/B measurements: agn_edge_forward's halves per wave (AGN_OPT_EDGE_FWD_HALVES)
-        nh = os.environ.get("AEROGNN_EDGE_FWD_HALVES")
-        if nh and L.agn_set_option(OPT_EDGE_FWD_HALVES, int(nh)) < 0:
-            raise AeroGNNError(f"AEROGNN_EDGE_FWD_HALVES={nh}: 1 or 2")
+        # A/B measurements: agn_edge_forward's halves per wave and waves per CU
+        # (AGN_OPT_EDGE_FWD_HALVES / _WAVES)
+        for env, key, ok in (("AEROGNN_EDGE_FWD_HALVES", OPT_EDGE_FWD_HALVES, "1 or 2"),
+                             ("AEROGNN_EDGE_FWD_WAVES", OPT_EDGE_FWD_WAVES, "12 or 16"),
+                             ("AEROGNN_EDGE_FWD32_WAVES", OPT_EDGE_FWD32_WAVES, "12 or 16"),
+                             ("AEROGNN_EDGE_FWD32_PRIO", OPT_EDGE_FWD32_PRIO, "0, 1 or 2")):
+            v = os.environ.get(env)
+            if v and L.agn_set_option(key, int(v)) < 0:
+                raise AeroGNNError(f"{env}={v}: {ok}")
     return _lib
 
 

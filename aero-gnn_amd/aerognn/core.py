@@ -329,14 +329,26 @@ def edge16_ok(dtype, hidden, nlin, has_ln, train):
     return (not train) or os.environ.get("AEROGNN_EDGE16_TRAIN", "0") == "1"
 
 
+def edge32_ok(dtype, hidden, nlin, has_ln, act=0):
+    """agn_edge_forward32 (csrc/edge32_fwd.hip) applies to the bf16 H=128 sum-trick ReLU edge chain
+    (W_e + 3 Linears + LN); AEROGNN_EDGE32=0 turns it off (then inference takes the 16-row forward,
+    training the resident agn_mlp_forward kernel, bitwise the same outputs as this one)."""
+    import os
+    return (os.environ.get("AEROGNN_EDGE32", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
+            and nlin == 4 and has_ln and act == 0)
+
+
 def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre=None, stats=None, tag=None,
-                 cost=None):
+                 cost=None, tiles32=False):
     """agn_edge_forward: out = e + LN(chain(e, P_s[src] + P_d[dst])); acts / hpre / stats are optional
-    row-major saves (parity tests only)."""
+    row-major saves (parity tests only). tiles32: agn_edge_forward32, the 32-row-tile kernel (no
+    saves; bitwise the resident agn_mlp_forward kernel)."""
     lib = L.lib()
+    if tiles32 and (acts is not None or hpre is not None or stats is not None):
+        raise L.AeroGNNError("agn_edge_forward32 writes no saves")
     a = L.EdgeFwdArgs()
     a.rows = int(rows)
-    a.nblk = int(lib.agn_edge_fwd_blocks(int(rows)))
+    a.nblk = int(lib.agn_edge_fwd32_blocks(int(rows)) if tiles32 else lib.agn_edge_fwd_blocks(int(rows)))
     for i in range(4):
         a.wpk[i] = wpk[i]
         a.bias[i] = bias[i]
@@ -346,7 +358,10 @@ def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre
         a.act[i] = ptr(acts[i]) if acts is not None else None
     a.hpre, a.stats = ptr(hpre), ptr(stats)
     with timed(tag, cost):
-        check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
+        if tiles32:
+            check(lib.agn_edge_forward32(C.byref(a), stream()), "edge_forward32")
+        else:
+            check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
 
 
 def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False,

@@ -23,7 +23,7 @@ from . import _lib as L
 from ._lib import check, ptr
 from . import core as _core
 from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
-                   edge16_ok, edge_forward,
+                   edge16_ok, edge32_ok, edge_forward,
                    cost_edge_bwd_fused,
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
@@ -400,6 +400,11 @@ class GMPFn(torch.autograd.Function):
         # the 16-row-tile pair (agn_edge_forward / agn_edge_backward) whenever no split-path saves
         # are needed: inference, and training with the fused backward
         e16 = spec.trick and (fused or not train) and edge16_ok(dt, H, es.nlin, es.ln is not None, train)
+        # the 32-row-tile forward (agn_edge_forward32, bitwise the resident agn_mlp_forward kernel the
+        # 32-row fused backward recomputes): inference and the fused training step, unless the
+        # 16-row pair trains or a parity test captures the 16-row kernel's saves
+        e32 = (spec.trick and (fused or not train) and not (train and e16) and _core.E16_SAVES is None
+               and edge32_ok(dt, H, es.nlin, es.ln is not None, es.act) and e.stride(0) == H)
         ea, ehp, est = _alloc_saves(es, E, dt, dev, train and not fused)
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         P = None
@@ -414,7 +419,13 @@ class GMPFn(torch.autograd.Function):
                             segs=[(L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None)],
                             wpk=[spec.pack["proj"]], bias=[spec.pack["proj_b"]], out=P,
                             tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
-            if e16:
+            if e32:
+                edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=level.src,
+                             dst=level.dst, out=e_out, tiles32=True,
+                             tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
+                                                                                                 False)))
+                e16 = False
+            elif e16:
                 # 16-row-tile kernel (csrc/edge16_fwd.hip); the fused backward recomputes it bitwise.
                 # core.E16_SAVES (parity tests only): also save a1..a3, h3 and the LN statistics
                 sv = None

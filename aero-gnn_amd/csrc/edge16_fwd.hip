@@ -19,19 +19,21 @@ namespace {
 
 // Variants: NH 16-row halves per wave (a 16 NH-row tile; gemm_fwd_n shares each weight fragment
 // read among the halves), NW waves per CU. NH = 1, NW = 16: four waves per SIMD at <= 128
-// registers; NH = 2, NW = 12: three per SIMD at <= 168, half the LDS reads per row.
-// agn_set_option(AGN_OPT_EDGE_FWD_HALVES) selects one.
+// registers; NH = 2: half the LDS reads per row, at NW = 12 (three per SIMD, <= 168 registers,
+// the residual operand kept) or NW = 16 (<= 128, the residual re-read from L2 in the epilogue).
+// agn_set_option(AGN_OPT_EDGE_FWD_HALVES / _WAVES) selects one.
 int g_fwd_nh = 2;
-template <int NH> constexpr int nw_of() { return NH == 1 ? 16 : 12; }
+int g_fwd_nw = 12;  // waves per CU for NH = 2
 
 constexpr int OFF_PV = 4 * IMG_B;                 // fp32 [5][H]: b1, b2, b3, LN gamma, LN beta
 constexpr int OFF_IDS = OFF_PV + 5 * H * 4;       // int [NW][2 * 16 NH]: next tile's src / dst
 template <int NH, int NW> constexpr int lds_bytes() { return OFF_IDS + NW * 2 * 16 * NH * 4; }
-static_assert(lds_bytes<1, nw_of<1>()>() <= 160 * 1024 && lds_bytes<2, nw_of<2>()>() <= 160 * 1024, "LDS budget");
+static_assert(lds_bytes<1, 16>() <= 160 * 1024 && lds_bytes<2, 16>() <= 160 * 1024, "LDS budget");
 
 template <int NH, int NW>
 __global__ __launch_bounds__(64 * NW) void edge16_fwd_kernel(const agn_edge_fwd_args a) {
   constexpr int NTHR = 64 * NW;
+  constexpr bool KEEP_E = NH == 1 || NW < 16;  // the residual operand kept from the first GEMM
   constexpr int TR = 16 * NH;  // rows per tile
   __shared__ __attribute__((aligned(16))) char lds[lds_bytes<NH, NW>()];
   load_images(lds, a.wpk, threadIdx.x, NTHR);
@@ -105,7 +107,11 @@ __global__ __launch_bounds__(64 * NW) void edge16_fwd_kernel(const agn_edge_fwd_
         a.stats[2 * (size_t)row[h]] = mean;
         a.stats[2 * (size_t)row[h] + 1] = rstd;
       }
-      // e' = e + round(gamma * xhat + beta), rounded again (the bf16 module's two roundings)
+      // e' = e + round(gamma * xhat + beta), rounded again (the bf16 module's two roundings); the
+      // residual is the kept operand, or (KEEP_E false: registers for a fourth wave per SIMD) e's
+      // row read again here (an L2 hit: the tile's first GEMM read it)
+      uint4 er[4];
+      if (!KEEP_E) load_raw(er, E + (size_t)(valid[h] ? row[h] : a.rows - 1) * H, lane);
       const float* gm = pv + 3 * H;
       const float* bt = pv + 4 * H;
       uint4 o[4];
@@ -123,7 +129,8 @@ __global__ __launch_bounds__(64 * NW) void edge16_fwd_kernel(const agn_edge_fwd_
             const f32x2 v = ln_out2(f2(acc[h][ob][e], acc[h][ob][e + 1]), mean, rstd, f2(g4[e], g4[e + 1]),
                                     f2(b4[e], b4[e + 1]));
             const uint32_t p = pack2(v[0], v[1]);
-            const f32x2 y = f2(lo_bf16(p), hi_bf16(p)) + f2(op_el(e0[h], ob, e), op_el(e0[h], ob, e + 1));
+            const f32x2 y = f2(lo_bf16(p), hi_bf16(p)) + (KEEP_E ? f2(op_el(e0[h], ob, e), op_el(e0[h], ob, e + 1))
+                                                                 : f2(raw_el(er, ob, e), raw_el(er, ob, e + 1)));
             wv[2 * hb + e / 2] = pack2(y[0], y[1]);
           }
         }
@@ -162,13 +169,20 @@ int edge16_fwd_set_halves(int nh) {
   g_fwd_nh = nh;
   return old;
 }
+// agn_set_option(AGN_OPT_EDGE_FWD_WAVES): waves per CU of the two-halves variant
+int edge16_fwd_set_waves(int nw) {
+  const int old = g_fwd_nw;
+  if (nw != 12 && nw != 16) return AGN_E_ARG;
+  g_fwd_nw = nw;
+  return old;
+}
 }  // namespace agn
 
 extern "C" {
 
 int agn_edge_fwd_blocks(int rows) {
   const int cus = cu_count();
-  const int nw = g_fwd_nh == 1 ? nw_of<1>() : nw_of<2>();
+  const int nw = g_fwd_nh == 1 ? 16 : g_fwd_nw;
   const int waves = (rows + 16 * g_fwd_nh - 1) / (16 * g_fwd_nh);
   const int need = (waves + nw - 1) / nw;
   if (need >= cus) return cus;
@@ -187,9 +201,11 @@ int agn_edge_forward(const agn_edge_fwd_args* a, void* stream) {
     if (!al16(a->act[l])) return AGN_E_ARG;
   if (!al16(a->hpre)) return AGN_E_ARG;
   if (g_fwd_nh == 1)
-    hipLaunchKernelGGL((edge16_fwd_kernel<1, nw_of<1>()>), dim3(a->nblk), dim3(64 * nw_of<1>()), 0, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL((edge16_fwd_kernel<1, 16>), dim3(a->nblk), dim3(64 * 16), 0, (hipStream_t)stream, *a);
+  else if (g_fwd_nw == 16)
+    hipLaunchKernelGGL((edge16_fwd_kernel<2, 16>), dim3(a->nblk), dim3(64 * 16), 0, (hipStream_t)stream, *a);
   else
-    hipLaunchKernelGGL((edge16_fwd_kernel<2, nw_of<2>()>), dim3(a->nblk), dim3(64 * nw_of<2>()), 0, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL((edge16_fwd_kernel<2, 12>), dim3(a->nblk), dim3(64 * 12), 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

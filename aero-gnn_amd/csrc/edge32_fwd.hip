@@ -1,0 +1,288 @@
+// Forward of the sum-trick edge MLP on 32-row tiles with 32x32x16 MFMAs (gfx950, bf16, H = 128):
+//   e' = e + LN(W3 relu(W2 relu(W1 relu(e W_e^T + P_s[src] + P_d[dst]) + b1) + b2) + b3)
+// (models/mgnLayer.py:72-105 EdgeBlockSum, residual :205), bitwise agn_mlp_forward's resident
+// kernel on the same operands (mlp.hip mlp_fwd_res_kernel: the same MFMA sequence per accumulator,
+// the same exact MFMA row sum P_s + P_d, the same LayerNorm and residual steps), so the 32-row
+// fused backward (edge_bwd.hip), which recomputes that kernel's chain, pairs with it unchanged.
+//
+// Why a second kernel: the chain is vector-issue-bound on the SIMD, not HBM- or MFMA-bound
+// (DESIGN.md §9 round 5). A v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its
+// 32 cycles, a 16x16x32 for 8 of 16: the 32-row tile halves the MFMA share of the issue budget
+// against edge16_fwd.hip, and the exact MFMA row sum replaces ~190 VALU unpack/add instructions
+// per tile. Against the resident kernel (two waves per SIMD at <= 256 registers, the previous
+// tile's stores deferred in registers) this one runs NW / 4 waves per SIMD: 12 waves at <= 168
+// registers keep the residual operand, 16 waves at <= 128 re-read it in the epilogue; the weight
+// fragments stream two deep instead of a whole k-step ahead.
+//
+// Persistent: one workgroup per CU, the four packed weight images resident in LDS (128 KB), each
+// wave streaming 32-row tiles in CSC order over an XCD-grouped walk; a tile's node ids are loaded
+// one tile ahead through the wave's LDS slot (a loop-carried load result would make the compiler
+// wait vmcnt(0) at the loop head, i.e. for the previous tile's stores too).
+#include "common.hpp"
+#include "aerognn.h"
+
+using namespace agn;
+
+namespace {
+
+constexpr int H = 128;
+constexpr int NT = 4;                   // 32-feature output tiles
+constexpr int NR = 64;                  // acc registers per lane (features of the lane's row half)
+constexpr int NU = 8;                   // k-steps of 16 per layer
+constexpr int LAYER = NT * NU * 64;     // packed units (16 B) per weight image
+#ifndef AGN_E32_PF
+#define AGN_E32_PF 2
+#endif
+constexpr int PF = AGN_E32_PF;          // weight fragments in flight
+
+int g_nw = 12;    // waves per CU (AGN_OPT_EDGE_FWD32_WAVES)
+int g_prio = 0;   // static wave priorities (AGN_OPT_EDGE_FWD32_PRIO)
+
+template <int NW> struct Smem {
+  uint4 w[4 * LAYER];   // packed A units [layer][ot][ku][lane] (agn_pack trans = 0 layout, as is)
+  float pv[5][H];       // b1, b2, b3, LN gamma, LN beta
+  int ids[NW][64];      // per wave: next tile's src (lanes 0-31) / dst (32-63)
+};
+static_assert(sizeof(Smem<16>) <= 160 * 1024, "LDS budget");
+
+// acc[ot] += W[ot tile] . b over k-steps u = 0..7 in order (the resident kernel's per-accumulator
+// sequence: common.hpp gemm); fragments (u, ot) stream PF deep, ot inner
+AGN_DEV void gemm4(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const uint4* w, int lane) {
+  uint4 f[PF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) f[i] = w[((i % NT) * NU + i / NT) * 64 + lane];
+#pragma unroll
+  for (int idx = 0; idx < NT * NU; ++idx) {
+    const uint4 cur = f[idx % PF];
+    const int nx = idx + PF;
+    if (nx < NT * NU) f[idx % PF] = w[((nx % NT) * NU + nx / NT) * 64 + lane];
+    b.mfma(acc[idx % NT], cur, idx / NT);
+  }
+}
+
+// XCD-aware walk (mlp.hip ResTiles): blocks b and b + 8 share an XCD and its L2, so each group of
+// blocks {g, g + 8, ...} walks one contiguous eighth of the tiles
+struct Walk {
+  int first, end, step;
+  AGN_DEV Walk(int ntiles, int w, int nw) {
+    if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
+      const int g = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = gridDim.x >> 3;
+      const int per = (ntiles + 7) / 8;
+      first = g * per + bi * nw + w;
+      end = min(ntiles, (g + 1) * per);
+      step = nb * nw;
+    } else {
+      first = blockIdx.x * nw + w;
+      end = ntiles;
+      step = gridDim.x * nw;
+    }
+  }
+};
+
+// s_setprio takes an immediate
+AGN_DEV void set_prio(int p) {
+  if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 3) __builtin_amdgcn_s_setprio(3);
+}
+
+template <int NW, int PRIO>
+__global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_args a) {
+  constexpr int NTHR = 64 * NW;
+  constexpr bool KEEP_E = NW <= 12;  // the residual: kept operand, or re-read in the epilogue
+  __shared__ Smem<NW> sm;
+  {
+    const uint4* const* wp = reinterpret_cast<const uint4* const*>(a.wpk);
+    for (int i = threadIdx.x; i < 4 * LAYER; i += NTHR) sm.w[i] = wp[i / LAYER][i % LAYER];
+    for (int i = threadIdx.x; i < 5 * H; i += NTHR) {
+      const int l = i / H, f = i - l * H;
+      sm.pv[l][f] = l < 3 ? (a.bias[l + 1] ? a.bias[l + 1][f] : 0.f) : (l == 3 ? a.ln_g[f] : a.ln_b[f]);
+    }
+  }
+  __syncthreads();
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // waves w, w + 4, w + 8 (, w + 12) share a SIMD (dispatched to the 4 SIMDs in turn): PRIO 1 ranks
+  // them by that order, PRIO 2 the reverse, so the three chains drift apart instead of running
+  // their MFMA and VALU phases in step (MI355X_MICROARCH.md, two waves per SIMD, items 4 and 9)
+  if constexpr (PRIO == 1) set_prio(w >> 2);
+  if constexpr (PRIO == 2) set_prio(NW / 4 - 1 - (w >> 2));
+  const int ntiles = (a.rows + 31) / 32;
+  const Walk walk(ntiles, w, NW);
+  int* wids = sm.ids[w];
+  const int32_t* const idp = lane0 < 32 ? a.src : a.dst;
+  auto tile_id = [&](int t) { return idp[min(t * 32 + (lane0 & 31), a.rows - 1)]; };
+  if (walk.first < walk.end) wids[lane0] = tile_id(walk.first);
+  const bf16* P = reinterpret_cast<const bf16*>(a.proj);
+  const bf16* E = reinterpret_cast<const bf16*>(a.e);
+  for (int tile = walk.first; tile < walk.end; tile += walk.step) {
+    cbarrier();
+    // lane-derived offsets recomputed per tile, not hoisted and kept live (common.hpp opaque_v)
+    const int lane = opaque_v(lane0);
+    const int c = lane & 31, h = lane >> 5;
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    const int rr = valid ? row : a.rows - 1;
+    const bool more = tile + walk.step < walk.end;
+    const int nid = tile_id(more ? tile + walk.step : tile);
+    f32x16 acc[NT];
+    BOp<bf16, NR> b;
+    {
+      const int cs = wids[c], cd = wids[32 + c];
+      if (more) wids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
+      // acc = P_s[src] + P_d[dst] on the matrix cores (exact fp32 add, common.hpp acc_add2_mfma)
+      BOp<bf16, NR> xs, xd;
+      uint4 rs[NR / 8], rd[NR / 8];
+      const bf16* ps = P + (size_t)cs * (2 * H) + 8 * h;
+      const bf16* pd = P + (size_t)cd * (2 * H) + H + 8 * h;
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        rs[i] = *reinterpret_cast<const uint4*>(ps + 16 * i);
+        rd[i] = *reinterpret_cast<const uint4*>(pd + 16 * i);
+      }
+      b.load_w(E + (size_t)rr * H, h);
+      xs.set_w(rs);
+      xd.set_w(rd);
+      bf16x8 f0, f1;
+      ident_frags(f0, f1, lane);
+      acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+    }
+    BOp<bf16, NR> e0;
+    if constexpr (KEEP_E) e0 = b;
+    gemm4(acc, b, sm.w, lane);
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+      cbarrier();
+      b.template set_relu<NT>(acc);
+#pragma unroll
+      for (int q = 0; q < 4 * NT; ++q) {  // acc = bias of Linear l (mlp.hip acc_bias_lds)
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&sm.pv[l - 1][8 * q + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+      }
+      gemm4(acc, b, sm.w + l * LAYER, lane);
+    }
+    cbarrier();
+    // LayerNorm statistics over the row's 128 features (two lanes per row), resident kernel order
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
+    s = sum32(s);
+    const float mean = s / (float)H;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NR; i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
+    q = sum32(q);
+    const float rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
+    const bf16* rp = E + (size_t)rr * H;
+    bf16* op = reinterpret_cast<bf16*>(a.out) + (size_t)row * H;
+#pragma unroll
+    for (int i = 0; i < NR / 8; ++i) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int f0 = 16 * i + 8 * j + 4 * h;
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(&sm.pv[3][f0]);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sm.pv[4][f0]);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2 o = ln_out2(f2(v[4 * j + e], v[4 * j + e + 1]), mean, rstd, f2(g4[e], g4[e + 1]),
+                                  f2(b4[e], b4[e + 1]));
+          v[4 * j + e] = o[0];
+          v[4 * j + e + 1] = o[1];
+        }
+      }
+      float r[8];
+      if constexpr (KEEP_E) e0.get8(r, i);
+      else load8_w(r, rp, i, h);
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {  // round(LN) + residual, rounded again at the store
+        const uint32_t p = pack2(v[e], v[e + 1]);
+        const f32x2 o = f2(lo_bf16(p), hi_bf16(p)) + f2(r[e], r[e + 1]);
+        v[e] = o[0];
+        v[e + 1] = o[1];
+      }
+      store8_w(op, i, h, v, valid);
+    }
+  }
+}
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int g_cus = 0;
+int cu_count() {
+  if (g_cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t pr;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&pr, dev) == hipSuccess) g_cus = pr.multiProcessorCount;
+    if (g_cus <= 0) g_cus = 256;
+  }
+  return g_cus;
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace
+
+namespace agn {
+// agn_set_option(AGN_OPT_EDGE_FWD32_WAVES / _PRIO) (mlp.hip)
+int edge32_fwd_set_option(int key, int value) {
+  if (key == AGN_OPT_EDGE_FWD32_WAVES) {
+    const int old = g_nw;
+    if (value != 12 && value != 16) return AGN_E_ARG;
+    g_nw = value;
+    return old;
+  }
+  if (key == AGN_OPT_EDGE_FWD32_PRIO) {
+    const int old = g_prio;
+    if (value < 0 || value > 2) return AGN_E_ARG;
+    g_prio = value;
+    return old;
+  }
+  return AGN_E_ARG;
+}
+}  // namespace agn
+
+namespace {
+template <int NW, int PRIO>
+void launch(const agn_edge_fwd_args* a, void* stream) {
+  hipLaunchKernelGGL((edge32_fwd_kernel<NW, PRIO>), dim3(a->nblk), dim3(64 * NW), 0, (hipStream_t)stream, *a);
+}
+template <int NW>
+void launch_p(const agn_edge_fwd_args* a, void* stream) {
+  if (g_prio == 1) launch<NW, 1>(a, stream);
+  else if (g_prio == 2) launch<NW, 2>(a, stream);
+  else launch<NW, 0>(a, stream);
+}
+}  // namespace
+
+extern "C" {
+
+int agn_edge_fwd32_blocks(int rows) {
+  const int cus = cu_count();
+  const int tiles = (rows + 31) / 32;
+  const int need = (tiles + g_nw - 1) / g_nw;
+  if (need >= cus) return cus;
+  const int n = (need + 7) / 8 * 8;
+  return n < 8 ? 8 : n;
+}
+
+int agn_edge_forward32(const agn_edge_fwd_args* a, void* stream) {
+  if (!a || a->rows < 0 || a->nblk < 1) return AGN_E_ARG;
+  if (a->rows == 0) return 0;
+  if (!a->e || !a->proj || !a->src || !a->dst || !a->out || !a->ln_g || !a->ln_b) return AGN_E_ARG;
+  if (a->act[0] || a->act[1] || a->act[2] || a->hpre || a->stats) return AGN_E_ARG;  // no saves
+  for (int l = 0; l < 4; ++l)
+    if (!a->wpk[l] || !al16(a->wpk[l])) return AGN_E_ARG;
+  if (!al16(a->e) || !al16(a->proj) || !al16(a->out)) return AGN_E_ARG;
+  if (g_nw == 16) launch_p<16>(a, stream);
+  else launch_p<12>(a, stream);
+  return launch_status();
+}
+
+}  // extern "C"

@@ -197,9 +197,19 @@ const char* agn_error_string(int code);
 /* Process-wide kernel-selection options (testing / A-B measurement). Returns the previous value
  * or AGN_E_ARG. AGN_OPT_RESIDENT: 1 (default) = persistent resident-weight kernels for the
  * large bf16 H=128 edge MLPs, 0 = always the general kernels (bitwise-identical outputs).
- * AGN_OPT_EDGE_FWD_HALVES: 16-row halves per wave of agn_edge_forward, 1 or 2 (default; bitwise-
- * identical outputs; agn_edge_fwd_blocks follows it). */
-enum { AGN_OPT_RESIDENT = 0, AGN_OPT_EDGE_FWD_HALVES = 1 };
+ * AGN_OPT_EDGE_FWD_HALVES: 16-row halves per wave of agn_edge_forward, 1 or 2 (default);
+ * AGN_OPT_EDGE_FWD_WAVES: waves per CU of the two-halves variant, 12 (default) or 16 (bitwise-
+ * identical outputs; agn_edge_fwd_blocks follows both).
+ * AGN_OPT_EDGE_FWD32_WAVES: waves per CU of agn_edge_forward32, 12 (default) or 16 (bitwise-
+ * identical outputs; agn_edge_fwd32_blocks follows it). AGN_OPT_EDGE_FWD32_PRIO: its static wave
+ * priorities, 0 = none, 1 = the k-th wave of each SIMD at priority k, 2 = the reverse. */
+enum {
+  AGN_OPT_RESIDENT = 0,
+  AGN_OPT_EDGE_FWD_HALVES = 1,
+  AGN_OPT_EDGE_FWD_WAVES = 2,
+  AGN_OPT_EDGE_FWD32_WAVES = 3,
+  AGN_OPT_EDGE_FWD32_PRIO = 4
+};
 int agn_set_option(int key, int value);
 /* bytes of a packed A operand with `m` rows and `k` reduction columns */
 size_t agn_packed_bytes(int m, int k, int dtype);
@@ -428,6 +438,13 @@ typedef struct {
 } agn_edge_fwd_args;
 int agn_edge_fwd_blocks(int rows);
 int agn_edge_forward(const agn_edge_fwd_args* a, void* stream);
+/* The same chain on 32-edge tiles with 32x32x16 MFMAs, bitwise agn_mlp_forward's resident kernel
+ * on the same operands (so agn_edge_bwd_fused's recompute pairs with it): the forward of the
+ * training step (fused backward) and of inference. No saves (act / hpre / stats must be NULL);
+ * grid agn_edge_fwd32_blocks(rows). Replaces mlp.py:37-60 MLP.forward on EdgeBlockSum's chain
+ * (mgnLayer.py:72-105) as agn_edge_forward does. */
+int agn_edge_fwd32_blocks(int rows);
+int agn_edge_forward32(const agn_edge_fwd_args* a, void* stream);
 int agn_edge_backward_blocks(int rows);
 int agn_edge_backward(const agn_edge_bwd_args* a, void* stream);
 /* dw[m][k] = sum_s dw_partial[s][m][k] (and db) for each desc: the fixed-order second stage

@@ -294,27 +294,79 @@ def test_edge16_backward_deterministic_and_close_to_round4_kernel():
 
 @pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (40000, 240000)])
 def test_edge16_forward_halves_bitwise(N, E):
-    """agn_edge_forward's two variants (one or two 16-row halves per wave, AGN_OPT_EDGE_FWD_HALVES)
-    give bitwise-equal outputs and saves: every accumulator sums the same products in the same order."""
+    """agn_edge_forward's variants (one or two 16-row halves per wave, AGN_OPT_EDGE_FWD_HALVES; 12
+    or 16 waves per CU for two, AGN_OPT_EDGE_FWD_WAVES, the latter re-reading the residual) give
+    bitwise-equal outputs and saves: every accumulator sums the same products in the same order."""
     from aerognn import _lib as L
     ch = Chain(18)
     src, dst = _level(N, E, 19)
     e, P, _, _ = _inputs(N, E, 20)
     lib = L.lib()
-    old = lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, 1)
+    old_h = lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, 1)
+    old_w = lib.agn_set_option(L.OPT_EDGE_FWD_WAVES, 12)
     try:
-        one = _forward(ch, e, P, src, dst)
+        runs = [_forward(ch, e, P, src, dst)]
         lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, 2)
-        two = _forward(ch, e, P, src, dst)
+        for nw in (12, 16):
+            lib.agn_set_option(L.OPT_EDGE_FWD_WAVES, nw)
+            runs.append(_forward(ch, e, P, src, dst))
     finally:
-        lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, old)
+        lib.agn_set_option(L.OPT_EDGE_FWD_HALVES, old_h)
+        lib.agn_set_option(L.OPT_EDGE_FWD_WAVES, old_w)
     torch.cuda.synchronize()
-    out1, acts1, hpre1, stats1 = one
-    out2, acts2, hpre2, stats2 = two
-    assert torch.equal(out1, out2)
-    for a1, a2 in zip(acts1, acts2):
-        assert torch.equal(a1, a2)
-    assert torch.equal(hpre1, hpre2) and torch.equal(stats1, stats2)
+    out1, acts1, hpre1, stats1 = runs[0]
+    for out2, acts2, hpre2, stats2 in runs[1:]:
+        assert torch.equal(out1, out2)
+        for a1, a2 in zip(acts1, acts2):
+            assert torch.equal(a1, a2)
+        assert torch.equal(hpre1, hpre2) and torch.equal(stats1, stats2)
+
+
+@pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (40000, 240000), (64, 32), (1000, 96)])
+def test_edge32_forward_bitwise_resident(N, E):
+    """agn_edge_forward32 (csrc/edge32_fwd.hip, 12 and 16 waves per CU) against agn_mlp_forward's
+    resident kernel on the same operands: bitwise (the same MFMA sequence per accumulator, the same
+    exact row sum and LayerNorm steps), which is what lets the 32-row fused backward's recompute
+    pair with it. Ragged tails (E % 32 != 0) and a single tile included."""
+    from aerognn import core
+    from aerognn import _lib as L
+    ch = Chain(21)
+    src, dst = _level(N, E, 22)
+    e, P, _, _ = _inputs(N, E, 23)
+    ref = torch.empty_like(e)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     ln=ch.spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=ref)
+    lib = L.lib()
+    old = lib.agn_set_option(L.OPT_EDGE_FWD32_WAVES, 12)
+    old_p = lib.agn_set_option(L.OPT_EDGE_FWD32_PRIO, 0)
+    outs = []
+    try:
+        for nw, prio in ((12, 0), (12, 1), (12, 2), (16, 0)):
+            lib.agn_set_option(L.OPT_EDGE_FWD32_WAVES, nw)
+            lib.agn_set_option(L.OPT_EDGE_FWD32_PRIO, prio)
+            out = torch.full_like(e, float("nan"))
+            core.edge_forward(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P,
+                              src=src, dst=dst, out=out, tiles32=True)
+            outs.append(out)
+    finally:
+        lib.agn_set_option(L.OPT_EDGE_FWD32_WAVES, old)
+        lib.agn_set_option(L.OPT_EDGE_FWD32_PRIO, old_p)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(ref.float()).all())
+    for out in outs:
+        assert torch.equal(out, ref)
+
+
+def test_edge32_forward_rejects_saves():
+    from aerognn import core
+    from aerognn import _lib as L
+    ch = Chain(24)
+    src, dst = _level(100, 300, 25)
+    e, P, _, _ = _inputs(100, 300, 26)
+    with pytest.raises(L.AeroGNNError):
+        core.edge_forward(rows=300, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P, src=src,
+                          dst=dst, out=torch.empty_like(e), hpre=torch.empty_like(e), tiles32=True)
 
 
 def test_edge16_forward_close_to_round4_kernel():
