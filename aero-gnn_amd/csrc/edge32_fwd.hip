@@ -34,6 +34,9 @@ constexpr int LAYER = NT * NU * 64;     // packed units (16 B) per weight image
 #define AGN_E32_PF 2
 #endif
 constexpr int PF = AGN_E32_PF;          // weight fragments in flight
+#ifndef AGN_E32_DIAG
+#define AGN_E32_DIAG 0  // timing diagnostics only (tools/fwd_probe.py): 1 no LayerNorm, 2 no residual, 3 no row sum
+#endif
 
 int g_nw = 12;    // waves per CU (AGN_OPT_EDGE_FWD32_WAVES)
 int g_prio = 0;   // static wave priorities (AGN_OPT_EDGE_FWD32_PRIO)
@@ -79,6 +82,23 @@ struct Walk {
   }
 };
 
+// Diagnostic phase clocks (built with -DAGN_E32_STAMPS into a separate library only,
+// tools/e32_stamps.py): the waves of block 0 record s_memtime at 8 points of their first 16 tiles
+// into agn_e32_stamps[(wave * 16 + tile) * 16 + point], s_memrealtime (100 MHz) at point 15.
+#ifdef AGN_E32_STAMPS
+__device__ unsigned long long* agn_e32_stamps;
+#define E32_STAMP(k)                                                                                   \
+  do {                                                                                                 \
+    if (agn_e32_stamps && blockIdx.x == 0 && lane0 == 0 && ntile < 16)                                 \
+      agn_e32_stamps[((threadIdx.x >> 6) * 16 + ntile) * 16 + (k)] =                                    \
+          (k) == 15 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();                   \
+  } while (0)
+#else
+#define E32_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
+
 // s_setprio takes an immediate
 AGN_DEV void set_prio(int p) {
   if (p == 1) __builtin_amdgcn_s_setprio(1);
@@ -115,8 +135,13 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
   if (walk.first < walk.end) wids[lane0] = tile_id(walk.first);
   const bf16* P = reinterpret_cast<const bf16*>(a.proj);
   const bf16* E = reinterpret_cast<const bf16*>(a.e);
+#ifdef AGN_E32_STAMPS
+  int ntile = 0;
+#endif
   for (int tile = walk.first; tile < walk.end; tile += walk.step) {
     cbarrier();
+    E32_STAMP(0);
+    E32_STAMP(15);
     // lane-derived offsets recomputed per tile, not hoisted and kept live (common.hpp opaque_v)
     const int lane = opaque_v(lane0);
     const int c = lane & 31, h = lane >> 5;
@@ -145,11 +170,21 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       xd.set_w(rd);
       bf16x8 f0, f1;
       ident_frags(f0, f1, lane);
-      acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+      if (AGN_E32_DIAG == 3) {
+#pragma unroll
+        for (int ot = 0; ot < NT; ++ot) {
+          acc[ot] = f32x16{};
+          acc[ot][0] = (float)xs.u[2 * ot][0] + (float)xd.u[2 * ot][0];
+        }
+      } else {
+        acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+      }
     }
+    E32_STAMP(1);
     BOp<bf16, NR> e0;
     if constexpr (KEEP_E) e0 = b;
     gemm4(acc, b, sm.w, lane);
+    E32_STAMP(2);
 #pragma unroll
     for (int l = 1; l < 4; ++l) {
       cbarrier();
@@ -161,19 +196,21 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
         for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
       }
       gemm4(acc, b, sm.w + l * LAYER, lane);
+      E32_STAMP(2 + l);
     }
     cbarrier();
     // LayerNorm statistics over the row's 128 features (two lanes per row), resident kernel order
     float s = 0.f;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
+    for (int i = 0; i < (AGN_E32_DIAG == 1 ? 1 : NR); ++i) s += acc[i / 16][i % 16];
     s = sum32(s);
     const float mean = s / (float)H;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < NR; i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
+    for (int i = 0; i < (AGN_E32_DIAG == 1 ? 2 : NR); i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
     q = sum32(q);
     const float rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
+    E32_STAMP(6);
     const bf16* rp = E + (size_t)rr * H;
     bf16* op = reinterpret_cast<bf16*>(a.out) + (size_t)row * H;
 #pragma unroll
@@ -182,7 +219,7 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < (AGN_E32_DIAG == 1 ? 0 : 2); ++j) {
         const int f0 = 16 * i + 8 * j + 4 * h;
         const f32x4 g4 = *reinterpret_cast<const f32x4*>(&sm.pv[3][f0]);
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sm.pv[4][f0]);
@@ -198,7 +235,7 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       if constexpr (KEEP_E) e0.get8(r, i);
       else load8_w(r, rp, i, h);
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {  // round(LN) + residual, rounded again at the store
+      for (int e = 0; e < (AGN_E32_DIAG == 2 ? 0 : 8); e += 2) {  // round(LN) + residual, rounded again at the store
         const uint32_t p = pack2(v[e], v[e + 1]);
         const f32x2 o = f2(lo_bf16(p), hi_bf16(p)) + f2(r[e], r[e + 1]);
         v[e] = o[0];
@@ -206,6 +243,10 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       }
       store8_w(op, i, h, v, valid);
     }
+    E32_STAMP(7);
+#ifdef AGN_E32_STAMPS
+    ++ntile;
+#endif
   }
 }
 
@@ -262,6 +303,12 @@ void launch_p(const agn_edge_fwd_args* a, void* stream) {
 }  // namespace
 
 extern "C" {
+
+#ifdef AGN_E32_STAMPS
+int agn_debug_e32_stamps(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(agn_e32_stamps), &p, sizeof(p)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int agn_edge_fwd32_blocks(int rows) {
   const int cus = cu_count();

@@ -1283,6 +1283,7 @@ namespace agn {
 int edge16_fwd_set_halves(int nh);  // edge16_fwd.hip
 int edge16_fwd_set_waves(int nw);   // edge16_fwd.hip
 int edge32_fwd_set_option(int key, int value);  // edge32_fwd.hip
+bool node32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);  // node32_fwd.hip
 }
 
 extern "C" {
@@ -1355,6 +1356,10 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
     else if (in_full && a->nlin > 1 && a->out_dim <= 32 && !a->use_ln) mode = M_NOUT;
   }
   const bool vec = mode == M_VEC;
+  if (g_opt_resident && vec) {  // a processor layer's node MLP: resident weights, aggregation walked in
+    int rc = 0;
+    if (agn::node32_fwd_try(a, stream, &rc)) return rc;
+  }
   if (res_fwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
     hipLaunchKernelGGL((mlp_fwd_res_kernel<bf16, 4>), g, dim3(RES_BLOCK), 0, (hipStream_t)stream, *a);
