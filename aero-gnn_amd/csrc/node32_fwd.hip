@@ -7,12 +7,15 @@
 // the x units then the agg units, the same LayerNorm and residual steps). agn_mlp_forward routes
 // such calls here (node32_fwd_try) unless AGN_OPT_RESIDENT is 0.
 //
-// Why: the general kernel restages every layer's weights into LDS for each 128-row block (1 KB of
-// weight staging per node row, more than the row's own 0.5-2 KB of HBM traffic). Here the three
-// packed weight images stay resident (128 KB: W0 is 128 x 256) and each of 12 waves per CU streams
-// 32-node tiles: the receiver rows' CSC offsets are prefetched a tile ahead through the wave's LDS
-// slot, the e' rows of each node are summed two rows in flight per lane (in two passes over the
-// row's halves), then the chain runs on the MFMA as edge32_fwd.hip's does.
+// Why: the general kernel restages every layer's weights into LDS for each 128-row block, and its
+// walk has each lane pair read its own node's rows, so one load instruction touches 32 rows (32-64
+// cache lines, 32 B of each). Here W0..W2 stay resident in LDS (128 KB: W0 is 128 x 256; a fourth
+// Linear's 32 KB stream from L2) and each of 8 waves per CU streams 32-node tiles: the receivers'
+// CSC offsets are prefetched a tile ahead through the wave's LDS slot, the e' rows are walked
+// coalesced (16 lanes per row, 4 rows per load instruction, 4 rows in flight per node), the rounded
+// sums reach the operand layout through a 2-KB LDS buffer, then the chain runs on the MFMA as
+// edge32_fwd.hip's does. C3 level-0 node MLP: 378 against 453 us per launch for the per-lane walk at
+// 12 waves (profiles/r5_node32_walk_ab.txt), 490 us for the general kernel.
 #include "common.hpp"
 #include "aerognn.h"
 
@@ -26,7 +29,14 @@ constexpr int NR = 64;
 constexpr int NU = 8;                     // k-steps of 16 per 128 input features
 constexpr int L0 = NT * 2 * NU * 64;      // W0 units (K = 256)
 constexpr int L1 = NT * NU * 64;          // W1 / W2 units
-constexpr int NW = 12;
+#ifndef AGN_N32_NW
+#define AGN_N32_NW 8
+#endif
+#ifndef AGN_N32_NQ
+#define AGN_N32_NQ 4
+#endif
+constexpr int NW = AGN_N32_NW;            // waves per CU (8: 256 registers for the walk's loads in flight)
+constexpr int NQ = AGN_N32_NQ;            // rows in flight per walked node
 constexpr int PF = 2;
 
 constexpr int PFG = 4;  // fragments in flight from L2 (the fourth Linear's weights)
@@ -37,6 +47,7 @@ template <int NLIN> struct Smem {
   uint4 w2[L1];          // (W3 of a four-Linear chain streams from L2: 160 KB do not fit beside the rest)
   float pv[NLIN + 2][H]; // b0 .. b_{NLIN-1}, LN gamma, LN beta
   int rp[NW][64];        // per wave: next tile's row pointers (33 used)
+  char agg[NW][2048];    // per wave: 8 nodes' rounded sums on their way to the owning lanes
 };
 static_assert(sizeof(Smem<4>) <= 160 * 1024, "LDS budget");
 
@@ -130,71 +141,97 @@ __global__ __launch_bounds__(64 * NW) void node32_fwd_kernel(const agn_mlp_fwd_a
     const int rr = valid ? row : a.rows - 1;
     const bool more = tile + walk.step < walk.end;
     const int nrp = tile_rp(more ? tile + walk.step : tile);
-    // ---- agg: the node's e' rows in edge order, fp32, one rounding (mlp.hip walk2_segment)
+    // ---- agg: each node's e' rows in edge order, fp32, one rounding (mlp.hip walk2_segment's
+    // values). The rows are read coalesced: lane group g = lane / 16 walks one node of a round,
+    // lane k = lane % 16 loads chunk k (16 B) of each of its rows, so one load instruction covers 4
+    // whole rows; two nodes per lane group (A, B) with up to 4 rows each in flight. The rounded sums
+    // reach the owning lanes (node c: lanes c and c + 32, the operand layout) through the wave's
+    // 2-KB LDS buffer, 8 nodes per batch.
     BOp<bf16, NR> bagg;
     {
-      // a partial last tile's rows past the end walk the last row's edges, as the general kernel
-      // does (its padding rows then carry the same values, mask bits included)
-      const int cc = valid ? c : a.rows - 1 - tile * 32;
-      const int beg = wrp[cc], end = wrp[cc + 1];
-      if (more) wrp[lane] = nrp;  // (this tile's reads of the slot are done: LDS is in order per wave)
-      // two passes over the row's chunks (4 of the lane's 8 each): 32 fp32 sums and two rows of 4
-      // chunks in flight fit beside the rest of the wave's registers (the whole row at once spills)
+      const int g = lane >> 4, k = lane & 15;
+      char* buf = sm.agg[w];
+      uint4 mine[NR / 8];
 #pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        float in[NR / 2];
+      for (int i = 0; i < NR / 8; ++i) mine[i] = uint4{0u, 0u, 0u, 0u};
+      const bf16* ek = EP + 8 * k;
+#pragma unroll 1
+      for (int bt = 0; bt < 4; ++bt) {
+        int beg[2], end[2];
 #pragma unroll
-        for (int i = 0; i < NR / 2; ++i) in[i] = 0.f;
-        const bf16* pb = EP + 64 * pass + 8 * h;
-        int j = beg;
-        for (; j + 1 < end; j += 2) {
-          uint4 r0[4], r1[4];
-          const bf16* p0 = pb + (size_t)j * sg.ld;
-          const bf16* p1 = p0 + sg.ld;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) r0[i] = *reinterpret_cast<const uint4*>(p0 + 16 * i);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) r1[i] = *reinterpret_cast<const uint4*>(p1 + 16 * i);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float o[8];
-            unpack8_w(o, r0[i]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) in[8 * i + e] += o[e];
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float o[8];
-            unpack8_w(o, r1[i]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) in[8 * i + e] += o[e];
-          }
+        for (int n = 0; n < 2; ++n) {
+          const int nl = 8 * bt + 4 * n + g;  // tile-local node
+          // a partial last tile's rows past the end walk the last row's edges, as the general
+          // kernel does (its padding rows then carry the same values, mask bits included)
+          const int cc = tile * 32 + nl < a.rows ? nl : a.rows - 1 - tile * 32;
+          beg[n] = wrp[cc];
+          end[n] = wrp[cc + 1];
         }
-        if (j < end) {
-          const bf16* p0 = pb + (size_t)j * sg.ld;
+        float sum[2][8];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float o[8];
-            unpack8_w(o, *reinterpret_cast<const uint4*>(p0 + 16 * i));
+        for (int n = 0; n < 2; ++n)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) in[8 * i + e] += o[e];
-          }
-        }
-        if (sg.kind == AGN_SEG_MEAN) {
-          const float cnt = (float)max(end - beg, 1);
+          for (int e = 0; e < 8; ++e) sum[n][e] = 0.f;
+        const int steps = max(end[0] - beg[0], end[1] - beg[1]);
+#pragma unroll 1
+        for (int j = 0; j < steps; j += NQ) {
+          uint4 r[2][NQ];
 #pragma unroll
-          for (int i = 0; i < NR / 2; ++i) in[i] = in[i] / cnt;
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+              if (beg[n] + j + q < end[n]) r[n][q] = *reinterpret_cast<const uint4*>(ek + (size_t)(beg[n] + j + q) * sg.ld);
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+              if (beg[n] + j + q < end[n]) {
+                const u32x4 x = __builtin_bit_cast(u32x4, r[n][q]);
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                  sum[n][2 * d] += lo_bf16(x[d]);
+                  sum[n][2 * d + 1] += hi_bf16(x[d]);
+                }
+              }
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {  // round once (BOp::set's pack), chunk 4 pass + i
-          float o[8];
+        for (int n = 0; n < 2; ++n) {
+          if (sg.kind == AGN_SEG_MEAN) {
+            const float cnt = (float)max(end[n] - beg[n], 1);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[e] = round_t<bf16>(in[8 * i + e]);
-          if (sg.store) store8_w(reinterpret_cast<bf16*>(sg.store) + (size_t)row * H, 4 * pass + i, h, o, valid);
-          bagg.u[4 * pass + i] = __builtin_bit_cast(bf16x8, u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]),
-                                                                 pack2(o[4], o[5]), pack2(o[6], o[7])});
+            for (int e = 0; e < 8; ++e) sum[n][e] = sum[n][e] / cnt;
+          }
+          const u32x4 pk = {pack2(sum[n][0], sum[n][1]), pack2(sum[n][2], sum[n][3]), pack2(sum[n][4], sum[n][5]),
+                            pack2(sum[n][6], sum[n][7])};
+          const int nl = 8 * bt + 4 * n + g;
+          if (sg.store && tile * 32 + nl < a.rows)
+            *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(sg.store) + (size_t)(tile * 32 + nl) * H + 8 * k) = pk;
+          *reinterpret_cast<u32x4*>(buf + (4 * n + g) * 256 + 16 * k) = pk;
+        }
+        // owners of this batch's nodes take their chunks (2i + h of their row) from the buffer
+        // (LDS is in order per wave: the reads see the writes above)
+        // (every lane reads, the owners keep: mine starts at 0 and each lane owns one batch's node)
+        const int nb = c - 8 * bt;
+        const uint32_t keep = (unsigned)nb < 8u ? ~0u : 0u;
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) {
+          const uint4 v = *reinterpret_cast<const uint4*>(buf + (nb & 7) * 256 + 16 * (2 * i + h));
+          mine[i].x |= v.x & keep;
+          mine[i].y |= v.y & keep;
+          mine[i].z |= v.z & keep;
+          mine[i].w |= v.w & keep;
         }
       }
+      if (more) wrp[lane] = nrp;  // (this tile's reads of the slot are done)
+      bagg.set_w(mine);
+      // the operand materialised here, before the x loads (else the two overlap and spill)
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        u32x4 t = __builtin_bit_cast(u32x4, bagg.u[i]);
+        asm volatile("" : "+v"(t));
+        bagg.u[i] = __builtin_bit_cast(bf16x8, t);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- layer 0: bias, then the x units, then the agg units. Row offsets are recomputed from an
     // opaque lane id here, not carried across the walk (where they would spill)
