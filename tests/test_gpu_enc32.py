@@ -1,0 +1,78 @@
+"""The resident encoder MLP forward on narrow rows (csrc/enc32_fwd.hip), which agn_mlp_forward
+picks for the node / edge encoders (k <= 16 input features, PLAIN or GATHER rows), against the
+general kernel's narrow-input mode (AGN_OPT_RESIDENT = 0) on the same operands: bitwise, with and
+without the training saves (mlp.py MLP, the encoders of models/bsms_mgn.py)."""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("AEROGNN_MEMLOG", "0")
+DEV = "cuda"
+H = 128
+
+
+class EncChain:
+    def __init__(self, seed, k, nlin):
+        from aerognn.core import Pack
+        from aerognn.functions import ChainSpec
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.nlin = nlin
+        self.w = [(torch.randn(H, k, generator=g) * k ** -0.5).to(DEV)] + \
+                 [(torch.randn(H, H, generator=g) * H ** -0.5).to(DEV) for _ in range(nlin - 1)]
+        self.b = [(torch.randn(H, generator=g) * 0.1).to(DEV) for _ in range(nlin)]
+        self.gamma = (1.0 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.beta = (0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.pack = Pack()
+        self.spec = ChainSpec(list(zip(self.w, self.b)), (self.gamma, self.beta), H, self.pack, "x")
+        self.pack.update(torch.bfloat16, torch.device(DEV))
+
+
+def _run(ch, x, idx, resident, saves):
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves
+    lib = L.lib()
+    n0 = lib.agn_debug_enc32_launches()
+    old = lib.agn_set_option(L.OPT_RESIDENT, int(resident))
+    rows = x.shape[0] if idx is None else idx.numel()
+    try:
+        out = torch.full((rows, H), float("nan"), dtype=torch.bfloat16, device=DEV)
+        acts = hpre = stats = None
+        if saves:
+            acts, hpre, stats = _alloc_saves(ch.spec, rows, torch.bfloat16, x.device, True)
+            for t in acts + [hpre, stats]:
+                t.zero_()
+            for t in acts:
+                t.agn_mask.zero_()
+        seg = (L.SEG_PLAIN, x.shape[1], x.stride(0), x, None, None) if idx is None else \
+            (L.SEG_GATHER, x.shape[1], x.stride(0), x, idx, None)
+        core.mlp_forward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=ch.nlin, out_dim=H, segs=[seg],
+                         wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), out=out,
+                         acts=acts, hpre=hpre, stats=stats)
+        torch.cuda.synchronize()
+    finally:
+        lib.agn_set_option(L.OPT_RESIDENT, old)
+    assert lib.agn_debug_enc32_launches() - n0 == int(resident)
+    sv = [] if not saves else [t for a in acts for t in (a, a.agn_mask)] + [hpre, stats]
+    return out, sv
+
+
+@pytest.mark.parametrize("rows,k,gather,nlin,saves", [
+    (400001, 4, True, 3, False), (70000, 6, False, 3, False), (65537, 4, False, 4, False),
+    (100000, 16, True, 3, True), (70001, 6, False, 3, True), (66000, 3, True, 4, True)])
+def test_enc32_bitwise_general(rows, k, gather, nlin, saves):
+    ch = EncChain(41, k, nlin)
+    g = torch.Generator(device="cpu").manual_seed(42)
+    n_in = rows + 123
+    x = torch.randn(n_in, k, generator=g).to(torch.bfloat16).to(DEV)
+    idx = torch.randperm(n_in, generator=g)[:rows].to(torch.int32).to(DEV) if gather else None
+    if not gather:
+        x = x[:rows]
+    ref, ref_sv = _run(ch, x, idx, False, saves)
+    out, sv = _run(ch, x, idx, True, saves)
+    assert bool(torch.isfinite(ref.float()).all())
+    assert torch.equal(out, ref)
+    for a, b in zip(sv, ref_sv):
+        assert torch.equal(a, b)
