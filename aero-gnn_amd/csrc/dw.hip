@@ -18,7 +18,10 @@ using namespace agn;
 
 namespace {
 
-constexpr int DW_ROWS = 64;   // rows per LDS stage
+#ifndef AGN_DW_ROWS
+#define AGN_DW_ROWS 64
+#endif
+constexpr int DW_ROWS = AGN_DW_ROWS;  // rows per LDS stage
 constexpr int DW_BLK = 128;   // output block edge
 constexpr int DW_THREADS = 256;
 

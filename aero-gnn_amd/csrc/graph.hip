@@ -138,6 +138,45 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int rows, int k, const
   }
 }
 
+// The same for 16-bit rows of exactly 8 * SEG_TPR features with 16-B aligned rows (the model's
+// H = 128 rows): up to 4 member rows per step, their indices loaded together and then their rows,
+// all in flight at once (the loop above waits for an index, then its row, every two rows); the
+// sum is the same sequence of fp32 adds in index order, so the result is bitwise the same
+constexpr int SEG_NQ = 4;
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sum4_kernel(int rows, const int32_t* __restrict__ ptr,
+                                                           const int32_t* __restrict__ perm, const T* __restrict__ src,
+                                                           int src_ld, T* __restrict__ out, int out_ld, int mean) {
+  constexpr int K = 8 * SEG_TPR;
+  const int f0 = 8 * (threadIdx.x & (SEG_TPR - 1));
+  const int r = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
+  if (r >= rows) return;
+  const int beg = ptr[r], end = ptr[r + 1];
+  using A_t = acc_of<T>;
+  A_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int j = beg; j < end; j += SEG_NQ) {
+    int e[SEG_NQ];
+#pragma unroll
+    for (int q = 0; q < SEG_NQ; ++q) e[q] = j + q < end ? (perm ? perm[j + q] : j + q) : -1;
+    A_t x[SEG_NQ][8];
+#pragma unroll
+    for (int q = 0; q < SEG_NQ; ++q)
+      if (e[q] >= 0) load8(x[q], src + (size_t)e[q] * src_ld, f0, K, true);
+#pragma unroll
+    for (int q = 0; q < SEG_NQ; ++q)
+      if (e[q] >= 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s[i] += x[q][i];
+      }
+  }
+  if (mean) {
+    const A_t cnt = (A_t)max(end - beg, 1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] /= cnt;
+  }
+  store8(out + (size_t)r * out_ld, f0, K, true, s);
+}
+
 // out[r] = (base[r] + (group a of r)) + (group b of r): the concat edge MLP's node gradient in one
 // pass (agn_segment_sum2). Same thread layout and in-order fp32 accumulation as segment_sum_kernel.
 template <typename T>
@@ -260,6 +299,53 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(int rows, int k, const
       for (int i = 0; i < 8; ++i) x[i] = rnd<T>(x[i]) + y[i];
     }
     store8(out + (size_t)r * out_ld, f0, k, vec, x);
+  }
+}
+
+// The same for 16-bit rows of exactly 8 * SEG_TPR features with 16-B aligned rows (the model's
+// H = 128 rows): each 16-lane group moves 4 rows, all loads issued before the first store, so a
+// wave keeps 4 KB in flight instead of 1 (same arithmetic per element: bitwise the kernel above)
+constexpr int GR_RPG = 4;  // rows per lane group
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows4_kernel(int rows, const int32_t* __restrict__ idx,
+                                                           const T* __restrict__ src, int src_ld,
+                                                           const int32_t* __restrict__ cnt_ptr,
+                                                           const T* __restrict__ add, int add_ld,
+                                                           T* __restrict__ out, int out_ld) {
+  constexpr int K = 8 * SEG_TPR;
+  const int f0 = 8 * (threadIdx.x & (SEG_TPR - 1));
+  const int ng = gridDim.x * (256 / SEG_TPR);
+  const int g = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
+  using A_t = acc_of<T>;
+  A_t x[GR_RPG][8], y[GR_RPG][8];
+  int s[GR_RPG];
+#pragma unroll
+  for (int i = 0; i < GR_RPG; ++i) {
+    const int r = g + i * ng;
+    s[i] = r < rows ? (idx ? idx[r] : r) : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < GR_RPG; ++i) {
+    const int r = g + i * ng;
+    if (s[i] >= 0) {
+      load8(x[i], src + (size_t)s[i] * src_ld, f0, K, true);
+      if (add) load8(y[i], add + (size_t)r * add_ld, f0, K, true);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < GR_RPG; ++i) {
+    const int r = g + i * ng;
+    if (s[i] < 0) continue;
+    if (cnt_ptr) {
+      const A_t div = (A_t)max(cnt_ptr[s[i] + 1] - cnt_ptr[s[i]], 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[i][e] /= div;
+    }
+    if (add) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[i][e] = rnd<T>(x[i][e]) + y[i][e];
+    }
+    store8(out + (size_t)r * out_ld, f0, K, true, x[i]);
   }
 }
 
@@ -687,6 +773,13 @@ __global__ void pool_emit_kernel(int nc, const int32_t* __restrict__ cand_ptr, c
 template <typename T>
 int seg_sum_t(int rows, int k, const int32_t* ptr, const int32_t* perm, const void* src, int src_ld, void* out,
               int out_ld, int mean, hipStream_t st) {
+  constexpr int A = 16 / sizeof(T);
+  if (sizeof(T) == 2 && k == 8 * SEG_TPR && src_ld % A == 0 && out_ld % A == 0 &&
+      ((((uintptr_t)src) | ((uintptr_t)out)) & 15) == 0) {
+    hipLaunchKernelGGL(segment_sum4_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, ptr, perm,
+                       (const T*)src, src_ld, (T*)out, out_ld, mean);
+    return launch_status();
+  }
   hipLaunchKernelGGL(segment_sum_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, ptr, perm,
                      (const T*)src, src_ld, (T*)out, out_ld, mean);
   return launch_status();
@@ -705,6 +798,14 @@ int seg_sum2_t(int rows, int k, const void* base, int base_ld, const int32_t* pt
 template <typename T>
 int gather_t(int rows, int k, const int32_t* idx, const void* src, int src_ld, const int32_t* cnt_ptr,
              const void* add, int add_ld, void* out, int out_ld, hipStream_t st) {
+  constexpr int A = 16 / sizeof(T);
+  if (sizeof(T) == 2 && k == 8 * SEG_TPR && src_ld % A == 0 && out_ld % A == 0 && (!add || add_ld % A == 0) &&
+      ((((uintptr_t)src) | ((uintptr_t)out) | ((uintptr_t)add)) & 15) == 0) {
+    const int groups = (rows + GR_RPG - 1) / GR_RPG;
+    hipLaunchKernelGGL(gather_rows4_kernel<T>, dim3((groups + 15) / 16), dim3(256), 0, st, rows, idx, (const T*)src,
+                       src_ld, cnt_ptr, (const T*)add, add_ld, (T*)out, out_ld);
+    return launch_status();
+  }
   hipLaunchKernelGGL(gather_rows_kernel<T>, dim3((rows + 15) / 16), dim3(256), 0, st, rows, k, idx, (const T*)src,
                      src_ld, cnt_ptr, (const T*)add, add_ld, (T*)out, out_ld);
   return launch_status();

@@ -171,6 +171,41 @@ def test_segment_sum_and_gather(dtype):
     assert rel_l2(o2.cpu(), ref2) <= tol
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("with_perm", [True, False])
+def test_segment_sum_and_gather_fast_paths_bitwise(dtype, with_perm):
+    """The 4-rows-in-flight kernels for 128-wide 16-bit rows (segment_sum4_kernel,
+    gather_rows4_kernel) against the general kernels, which an output row stride that is not a
+    multiple of 8 elements selects: bitwise (the same fp32 adds in index order)."""
+    from aerognn.core import gather_rows, segment_sum
+    g = torch.Generator(device="cpu").manual_seed(7)
+    rows, n_src, k = 70001, 300000, 128
+    counts = torch.randint(0, 14, (rows,), generator=g)
+    counts[::13] = 0
+    counts[5] = 300
+    ptr = torch.zeros(rows + 1, dtype=torch.int32)
+    ptr[1:] = torch.cumsum(counts, 0)
+    tot = int(ptr[-1])
+    perm = torch.randint(0, n_src, (tot,), generator=g, dtype=torch.int32).to(DEV) if with_perm else None
+    src = torch.randn(n_src if with_perm else tot, k, generator=g).to(dtype).to(DEV)
+    for mean in (False, True):
+        fast = torch.empty(rows, k, dtype=dtype, device=DEV)
+        gen = torch.empty(rows, k + 2, dtype=dtype, device=DEV)[:, :k]
+        segment_sum(rows, k, ptr.to(DEV), perm, src, fast, mean=mean)
+        segment_sum(rows, k, ptr.to(DEV), perm, src, gen, mean=mean)
+        torch.cuda.synchronize()
+        assert torch.equal(fast, gen)
+    idx = torch.randint(0, rows, (100003,), generator=g, dtype=torch.int32).to(DEV)
+    add = torch.randn(100003, k, generator=g).to(dtype).to(DEV)
+    for cnt, ad in ((None, None), (ptr.to(DEV), add)):
+        o_fast = torch.empty(100003, k, dtype=dtype, device=DEV)
+        o_gen = torch.empty(100003, k + 2, dtype=dtype, device=DEV)[:, :k]
+        gather_rows(100003, k, idx, fast, o_fast, cnt_ptr=cnt, add=ad)
+        gather_rows(100003, k, idx, fast, o_gen, cnt_ptr=cnt, add=ad)
+        torch.cuda.synchronize()
+        assert torch.equal(o_fast, o_gen)
+
+
 @pytest.mark.parametrize("n", [1, 5, 4096, 4097, 300001, 2_000_000])
 def test_exclusive_scan(n):
     from aerognn.graph import exclusive_scan
