@@ -1285,6 +1285,7 @@ int edge16_fwd_set_waves(int nw);   // edge16_fwd.hip
 int edge32_fwd_set_option(int key, int value);  // edge32_fwd.hip
 bool node32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);  // node32_fwd.hip
 bool enc32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
+bool node32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc, int* ln_rows);  // node32_bwd.hip
 }
 
 extern "C" {
@@ -1397,6 +1398,13 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
   }
   const bool vec = mode == M_VEC;
   agn_mlp_bwd_args* am = const_cast<agn_mlp_bwd_args*>(a);
+  if (g_opt_resident && vec) {  // a processor layer's node MLP: resident weights
+    int rc = 0, lr = 0;
+    if (agn::node32_bwd_try(a, stream, &rc, &lr)) {
+      am->ln_rows = lr;
+      return rc;
+    }
+  }
   if (res_bwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));
     am->ln_rows = (int)g.x;

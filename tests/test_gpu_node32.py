@@ -111,3 +111,51 @@ def test_node32_training_saves_bitwise_general(N, deg, nlin):
     assert len(sv) == 2 * (nlin - 1) + 2
     for a, b in zip(sv, ref_sv):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,deg", [(70000, 6), (65601, 3)])
+def test_node32_backward_bitwise_general(N, deg):
+    """The resident node MLP backward (csrc/node32_bwd.hip, picked inside agn_mlp_backward) against
+    the general kernel (AGN_OPT_RESIDENT = 0) on the forward's own saves: the pre-activation
+    gradients G_3..G_0 (AGN_TILED), dx (+ the residual's g), dagg and the LayerNorm partial rows,
+    bitwise; a partial last tile and a partial last 128-row block included."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_gpre
+    ch = NodeChain(51, 4)
+    E = N * deg
+    rowptr = _graph(N, E, 52, 0.1)
+    g = torch.Generator(device="cpu").manual_seed(53)
+    x = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    ep = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    gx = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    _, agg, sv = _run(ch, x, ep, rowptr, L.SEG_SUM, True, True, saves=True)
+    acts = [sv[0], sv[2], sv[4]]
+    hpre, stats = sv[6], sv[7]
+    lib = L.lib()
+    res = []
+    for resident in (False, True):
+        n0 = lib.agn_debug_node32_bwd_launches()
+        old = lib.agn_set_option(L.OPT_RESIDENT, int(resident))
+        try:
+            gpre = _alloc_gpre(ch.spec, N, torch.bfloat16, x.device)
+            for t in gpre:
+                t.zero_()
+            dx = torch.full_like(x, float("nan"))
+            dagg = torch.full_like(x, float("nan"))
+            part = torch.full((core.bwd_nblocks(N), 2 * H), float("nan"), dtype=torch.float32, device=DEV)
+            nb = core.mlp_backward(rows=N, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H, in_dim=2 * H,
+                                   wtpk=ch.spec.wtpk(), acts=acts, g=gx, gpre=gpre, ln_g=ch.spec.lnp()[0],
+                                   hpre=hpre, stats=stats, din=[(H, dx, True), (H, dagg, False)], ln_partial=part)
+            torch.cuda.synchronize()
+        finally:
+            lib.agn_set_option(L.OPT_RESIDENT, old)
+        assert lib.agn_debug_node32_bwd_launches() - n0 == int(resident)
+        res.append((nb, gpre, dx, dagg, part))
+    (nb0, gp0, dx0, da0, p0), (nb1, gp1, dx1, da1, p1) = res
+    assert nb0 == nb1 == core.bwd_nblocks(N)
+    assert bool(torch.isfinite(dx0.float()).all()) and bool(torch.isfinite(p0).all())
+    assert torch.equal(dx1, dx0) and torch.equal(da1, da0)
+    for a, b in zip(gp1, gp0):
+        assert torch.equal(a, b)
+    assert torch.equal(p1, p0)
