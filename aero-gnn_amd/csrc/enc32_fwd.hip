@@ -191,6 +191,78 @@ __global__ __launch_bounds__(64 * NW) void enc32_fwd_kernel(const agn_mlp_fwd_ar
   }
 }
 
+// The decoder (mlp.py MLP on H-wide rows to <= 32 outputs, no LayerNorm; models/bsms_mgn.py
+// decoder) at inference, bitwise the general kernel's narrow-output mode (mlp.hip M_NOUT: the last
+// Linear computes output tile 0 only, its bias masked to out_dim): weights resident, 16 waves per CU.
+template <int NLIN> struct DecSmem {
+  uint4 w[NLIN][LW];      // the last image holds output tile 0 only (its first NU * 64 units)
+  float pv[NLIN][H];
+};
+static_assert(sizeof(DecSmem<4>) <= 160 * 1024, "LDS budget");
+
+template <int NLIN>
+__global__ __launch_bounds__(64 * NW) void dec32_fwd_kernel(const agn_mlp_fwd_args a) {
+  constexpr int NTHR = 64 * NW;
+  __shared__ DecSmem<NLIN> sm;
+  for (int l = 0; l < NLIN; ++l) {
+    const uint4* wl = reinterpret_cast<const uint4*>(a.wpk[l]);
+    const int n = l < NLIN - 1 ? LW : NU * 64;
+    for (int i = threadIdx.x; i < n; i += NTHR) sm.w[l][i] = wl[i];
+  }
+  for (int i = threadIdx.x; i < NLIN * H; i += NTHR) {
+    const int l = i / H, f = i - l * H;
+    sm.pv[l][f] = (a.bias[l] && (l < NLIN - 1 || f < a.out_dim)) ? a.bias[l][f] : 0.f;
+  }
+  __syncthreads();
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntiles = (a.rows + 31) / 32;
+  const Walk walk(ntiles, w);
+  const agn_seg& sx = a.seg[0];
+  const bf16* X = reinterpret_cast<const bf16*>(sx.ptr);
+  for (int tile = walk.first; tile < walk.end; tile += walk.step) {
+    cbarrier();
+    const int lane = opaque_v(lane0);
+    const int c = lane & 31, h = lane >> 5;
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    const int rr = valid ? row : a.rows - 1;
+    BOp<bf16, NR> b;
+    b.load_w(X + (size_t)rr * sx.ld, h);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int q = 0; q < 4 * NT; ++q) {
+      const f32x4 x = *reinterpret_cast<const f32x4*>(&sm.pv[0][8 * q + 4 * h]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+    }
+    gemm_k8(acc, b, sm.w[0], lane);
+#pragma unroll
+    for (int l = 1; l < NLIN; ++l) {
+      cbarrier();
+      b.template set_relu<NT>(acc);
+#pragma unroll
+      for (int q = 0; q < 4 * NT; ++q) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&sm.pv[l][8 * q + 4 * h]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+      }
+      if (l < NLIN - 1) {
+        gemm_k8(acc, b, sm.w[l], lane);
+      } else {  // output tile 0 only, k-steps in order
+#pragma unroll
+        for (int u = 0; u < NU; ++u) b.mfma(acc[0], sm.w[l][u * 64 + lane], u);
+      }
+    }
+    bf16* op = reinterpret_cast<bf16*>(a.out) + (size_t)row * a.out_ld;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = {acc[0][4 * q], acc[0][4 * q + 1], acc[0][4 * q + 2], acc[0][4 * q + 3]};
+      if (valid) store4_masked(op, 8 * q + 4 * h, a.out_dim, false, v);
+    }
+  }
+}
+
 int g_cus = 0;
 int cu_count() {
   if (g_cus == 0) {
@@ -205,10 +277,12 @@ int cu_count() {
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 long g_launches = 0;
+long g_dec_launches = 0;
 
 }  // namespace
 
 extern "C" long agn_debug_enc32_launches(void) { return g_launches; }
+extern "C" long agn_debug_dec32_launches(void) { return g_dec_launches; }
 
 namespace agn {
 // agn_mlp_forward (mlp.hip) hands over the narrow-input encoder MLPs this kernel covers: returns
@@ -244,6 +318,33 @@ bool enc32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc) {
     else hipLaunchKernelGGL((enc32_fwd_kernel<3, false>), g, blk, 0, st, *a);
   }
   ++g_launches;
+  const hipError_t e = hipGetLastError();
+  *rc = e == hipSuccess ? 0 : (int)e;
+  return true;
+}
+// the decoder: agn_mlp_forward's narrow-output calls (M_NOUT) this kernel covers
+bool dec32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc) {
+  if (a->dtype != AGN_BF16 || a->hidden != H || (a->nlin != 3 && a->nlin != 4) || a->nseg != 1 || a->out_dim > 32 ||
+      a->out_dim < 1 || a->use_ln || a->act_fn != AGN_ACT_RELU || a->proj || a->resid || a->rows < 64 * 1024)
+    return false;
+  const agn_seg& sx = a->seg[0];
+  if (sx.kind != AGN_SEG_PLAIN || sx.k != H || sx.ld % 8 || !sx.ptr || !al16(sx.ptr)) return false;
+  // inference only: with the training saves this kernel spills at 128 registers and measured slower
+  // than the general kernel (the decoder is one launch per step either way)
+  for (int l = 0; l < AGN_MAX_LIN; ++l)
+    if (a->pre[l] || a->act[l] || a->mask[l]) return false;
+  if (a->hpre || a->stats) return false;
+  for (int l = 0; l < a->nlin; ++l)
+    if (!a->wpk[l] || !al16(a->wpk[l])) return false;
+  const int tiles = (a->rows + 31) / 32;
+  const int need = (tiles + NW - 1) / NW;
+  const int cus = cu_count();
+  const int nblk = need >= cus ? cus : ((need + 7) / 8 * 8 < 8 ? 8 : (need + 7) / 8 * 8);
+  const dim3 g(nblk), blk(64 * NW);
+  hipStream_t st = (hipStream_t)stream;
+  if (a->nlin == 4) hipLaunchKernelGGL((dec32_fwd_kernel<4>), g, blk, 0, st, *a);
+  else hipLaunchKernelGGL((dec32_fwd_kernel<3>), g, blk, 0, st, *a);
+  ++g_dec_launches;
   const hipError_t e = hipGetLastError();
   *rc = e == hipSuccess ? 0 : (int)e;
   return true;

@@ -1285,6 +1285,7 @@ int edge16_fwd_set_waves(int nw);   // edge16_fwd.hip
 int edge32_fwd_set_option(int key, int value);  // edge32_fwd.hip
 bool node32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);  // node32_fwd.hip
 bool enc32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
+bool dec32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
 bool node32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc, int* ln_rows);  // node32_bwd.hip
 }
 
@@ -1365,6 +1366,10 @@ int agn_mlp_forward(const agn_mlp_fwd_args* a, void* stream) {
   if (g_opt_resident && mode == M_NIN) {  // an encoder on narrow rows: resident weights
     int rc = 0;
     if (agn::enc32_fwd_try(a, stream, &rc)) return rc;
+  }
+  if (g_opt_resident && mode == M_NOUT) {  // the decoder to <= 32 outputs: resident weights
+    int rc = 0;
+    if (agn::dec32_fwd_try(a, stream, &rc)) return rc;
   }
   if (res_fwd_ok(a, vec)) {
     dim3 g(res_blocks(a->rows));

@@ -76,3 +76,50 @@ def test_enc32_bitwise_general(rows, k, gather, nlin, saves):
     assert torch.equal(out, ref)
     for a, b in zip(sv, ref_sv):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows,out_dim,nlin,saves", [(70000, 3, 4, False), (65537, 4, 3, True), (100001, 32, 4, True)])
+def test_dec32_bitwise_general(rows, out_dim, nlin, saves):
+    """The resident decoder forward (dec32_fwd_kernel: H-wide rows to <= 32 outputs, no LayerNorm)
+    against the general kernel's narrow-output mode, bitwise; with training saves agn_mlp_forward
+    keeps the general kernel (checked through the launch counter)."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.core import Pack
+    from aerognn.functions import ChainSpec, _alloc_saves
+    g = torch.Generator(device="cpu").manual_seed(61)
+    ws = [(torch.randn(H, H, generator=g) * H ** -0.5).to(DEV) for _ in range(nlin - 1)] + \
+         [(torch.randn(out_dim, H, generator=g) * H ** -0.5).to(DEV)]
+    bs = [(torch.randn(H, generator=g) * 0.1).to(DEV) for _ in range(nlin - 1)] + \
+         [(torch.randn(out_dim, generator=g) * 0.1).to(DEV)]
+    pack = Pack()
+    spec = ChainSpec(list(zip(ws, bs)), None, H, pack, "d")
+    pack.update(torch.bfloat16, torch.device(DEV))
+    x = torch.randn(rows, H, generator=g).to(torch.bfloat16).to(DEV)
+    lib = L.lib()
+    res = []
+    for resident in (False, True):
+        n0 = lib.agn_debug_dec32_launches()
+        old = lib.agn_set_option(L.OPT_RESIDENT, int(resident))
+        try:
+            out = torch.full((rows, out_dim), float("nan"), dtype=torch.bfloat16, device=DEV)
+            acts = None
+            if saves:
+                acts, _, _ = _alloc_saves(spec, rows, torch.bfloat16, x.device, True)
+                for t in acts:
+                    t.zero_()
+                    t.agn_mask.zero_()
+            core.mlp_forward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=nlin, out_dim=out_dim,
+                             segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None)], wpk=spec.wpk(),
+                             bias=spec.biases(), out=out, acts=acts)
+            torch.cuda.synchronize()
+        finally:
+            lib.agn_set_option(L.OPT_RESIDENT, old)
+        # the resident decoder serves inference only (training saves: the general kernel)
+        assert lib.agn_debug_dec32_launches() - n0 == int(resident and not saves)
+        res.append((out, [] if acts is None else [t for a in acts for t in (a, a.agn_mask)]))
+    (o0, s0), (o1, s1) = res
+    assert bool(torch.isfinite(o0.float()).all())
+    assert torch.equal(o1, o0)
+    for a, b in zip(s1, s0):
+        assert torch.equal(a, b)
