@@ -318,10 +318,11 @@ def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
 
 def edge16_ok(dtype, hidden, nlin, has_ln, train):
     """The 16-row-tile edge chain kernels (csrc/edge16*.hip: agn_edge_forward / agn_edge_backward)
-    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). Inference uses the 16-row
-    forward (AEROGNN_EDGE16=0 turns it off). Training keeps the 32-row pair (agn_mlp_forward's
-    resident kernel + agn_edge_bwd_fused, bitwise-consistent recompute) unless AEROGNN_EDGE16_TRAIN=1:
-    the 16-row fused backward measured slower."""
+    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). Inference takes the 32-row
+    forward (agn_edge_forward32, edge32_ok) first, the 16-row one with AEROGNN_EDGE32=0
+    (AEROGNN_EDGE16=0 turns this one off too). Training keeps the 32-row pair (agn_edge_forward32,
+    bitwise the resident agn_mlp_forward kernel, + agn_edge_bwd_fused) unless
+    AEROGNN_EDGE16_TRAIN=1: the 16-row fused backward measured slower."""
     import os
     if not (os.environ.get("AEROGNN_EDGE16", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
             and nlin == 4 and has_ln):
