@@ -242,6 +242,7 @@ def lib():
             "agn_edge_backward_blocks": (i32, [i32]),
             "agn_edge_backward": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_fault_status": (i32, [C.POINTER(i32), i32]),
+            "agn_fault_status_async": (i32, [vp, vp]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_proj_forward": (i32, [i32, vp, i32, vp, vp, vp, i32, vp]),
             "agn_proj_backward": (i32, [i32, vp, vp, i32, vp, vp, i32, vp]),

@@ -365,6 +365,34 @@ def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre
             check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
 
 
+# Production-path fault polling: every FAULT_POLL_EVERY fused launches an async copy
+# of the device fault words goes to page-locked host memory (agn_fault_status_async, no device
+# synchronisation); a later launch reads it once the copy's event has completed, so a ring
+# timeout raises at most a step or two after it happened instead of leaving wrong dW silently.
+FAULT_POLL_EVERY = 16
+_fault = {"buf": None, "event": None, "n": 0}
+
+
+def _poll_faults():
+    st = _fault
+    ev = st["event"]
+    if ev is not None and ev.query():
+        f = int(st["buf"][0]) | int(st["buf"][1])
+        st["event"] = None
+        if f:
+            raise L.AeroGNNError(f"fused edge backward: device fault word {f:#x} (LDS ring wait timed out; "
+                                 "dW of a recent step invalid)")
+    st["n"] += 1
+    if st["event"] is None and st["n"] >= FAULT_POLL_EVERY:
+        st["n"] = 0
+        if st["buf"] is None:
+            st["buf"] = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        check(L.lib().agn_fault_status_async(C.c_void_p(st["buf"].data_ptr()), stream()), "fault_status_async")
+        ev = torch.cuda.Event()
+        ev.record()
+        st["event"] = ev
+
+
 def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False,
                    dpd=None, rowptr=None):
     """agn_edge_backward (e16, the 16-row-tile kernel) or agn_edge_bwd_fused (the 32-row kernel);
@@ -402,6 +430,8 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
         f = L.fault_status(reset=True)
         if f:
             raise L.AeroGNNError(f"agn_edge_bwd_fused: device fault word {f:#x} (LDS ring wait timed out; dW invalid)")
+    else:
+        _poll_faults()
     dw = torch.empty(3, H, H, dtype=torch.float32, device=dev)
     db = torch.empty(3, H, dtype=torch.float32, device=dev)
     b = L.WgradBatch()

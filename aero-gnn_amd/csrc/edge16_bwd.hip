@@ -540,6 +540,13 @@ int agn_edge_backward_blocks(int rows) {
 }
 
 // this code object's fault word (agn_fault_status ORs it into the reported value)
+// (agn_fault_status_async, edge_bwd.hip)
+int agn_e16_fault_status_async(int* host_pinned, void* stream) {
+  const hipError_t e = hipMemcpyFromSymbolAsync(host_pinned, HIP_SYMBOL(g_e16_fault), sizeof(int), 0,
+                                                hipMemcpyDeviceToHost, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : (int)e;
+}
+
 int agn_e16_fault_status(int* value, int reset) {
   if (!value) return AGN_E_ARG;
   hipError_t e = hipDeviceSynchronize();

@@ -1039,6 +1039,15 @@ int agn_edge_bwd_blocks(int rows) {
 }
 
 int agn_e16_fault_status(int* value, int reset);
+int agn_e16_fault_status_async(int* host_pinned, void* stream);
+int agn_fault_status_async(int* host_pinned, void* stream) {
+  if (!host_pinned) return AGN_E_ARG;
+  const hipError_t e = hipMemcpyFromSymbolAsync(host_pinned, HIP_SYMBOL(g_agn_fault), sizeof(int), 0,
+                                                hipMemcpyDeviceToHost, (hipStream_t)stream);
+  if (e != hipSuccess) return (int)e;
+  return agn_e16_fault_status_async(host_pinned + 1, stream);
+}
+
 int agn_fault_status(int* value, int reset) {
   if (!value) return AGN_E_ARG;
   hipError_t e = hipDeviceSynchronize();

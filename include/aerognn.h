@@ -410,6 +410,11 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
  * up and that launch's dW / db are wrong. Synchronises the device; reset != 0 clears the word. */
 #define AGN_FAULT_RING_TIMEOUT 1
 int agn_fault_status(int* value, int reset);
+/* The same words without a device synchronisation: enqueues on `stream` copies of the fault word
+ * of agn_edge_bwd_fused (to host_pinned[0]) and of agn_edge_backward (host_pinned[1]) into
+ * page-locked host memory; the values are valid once the stream reaches the copies. Nothing is
+ * reset. The production path polls this once per step (aerognn/core.py). */
+int agn_fault_status_async(int* host_pinned, void* stream);
 /* ---- 16-row-tile sum-trick edge chain (bf16, H = 128; csrc/edge16*.hip) ----
  * The same EdgeBlockSum chain (mgnLayer.py:72-105, residual :205) on v_mfma_f32_16x16x32_bf16
  * 16-edge tiles: the forward keeps four waves per SIMD, and the fused backward two chain waves

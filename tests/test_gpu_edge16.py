@@ -385,3 +385,25 @@ def test_edge16_forward_close_to_round4_kernel():
     r = rel_l2(out.double(), old.double())
     print(f"edge16 vs round-4 resident forward e': rel-L2 {r:.2e}")
     assert r <= 5e-3
+
+
+def test_fault_status_async_reads_words():
+    """agn_fault_status_async (the production path's poll, aerognn/core.py _poll_faults): copies
+    both fused backwards' fault words to page-locked host memory without a device sync."""
+    import ctypes as C
+    from aerognn import _lib as L
+    from aerognn import core
+    assert L.fault_status(reset=True) == 0
+    buf = torch.full((2,), -1, dtype=torch.int32, pin_memory=True)
+    core.check(L.lib().agn_fault_status_async(C.c_void_p(buf.data_ptr()), core.stream()), "fault_status_async")
+    torch.cuda.synchronize()
+    assert buf.tolist() == [0, 0]
+    # the poll itself: FAULT_POLL_EVERY calls enqueue one copy, a later call reads it
+    old = core.FAULT_POLL_EVERY
+    core.FAULT_POLL_EVERY = 1
+    try:
+        core._poll_faults()
+        torch.cuda.synchronize()
+        core._poll_faults()
+    finally:
+        core.FAULT_POLL_EVERY = old
