@@ -269,34 +269,48 @@ __global__ __launch_bounds__(DW_THREADS) void wgrad_kernel(const agn_wgrad_batch
   }
 }
 
-// out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns 64 column quads (256
+// out[m][k] = sum_s partial[s][m][k] (m < M, k < K). A block owns RED_Q column quads (4 RED_Q
 // floats of the [mpad][kpad] slab); its RED_G thread groups each sum the splits s = g,
 // g + RED_G, ... and the group partials are combined in LDS in group order: a fixed
-// summation order (deterministic), with RED_G x 64 16-B loads in flight per block.
+// summation order (deterministic), with RED_G x RED_Q 16-B loads in flight per block. RED_Q = 16
+// spreads a 128 x 128 slab over 256 blocks (64 quads per block left 3/4 of the CUs idle: the
+// reduce of a 768-split slab ran at ~1.5 TB/s)
 constexpr int RED_G = 8;
-__global__ __launch_bounds__(64 * RED_G) void wgrad_reduce_kernel(const agn_wgrad_batch b) {
-  __shared__ f32x4 part[RED_G][64];
-  __shared__ float bpart[RED_G][64];
+constexpr int RED_Q = 16;
+__global__ __launch_bounds__(RED_Q * RED_G) void wgrad_reduce_kernel(const agn_wgrad_batch b) {
+  __shared__ f32x4 part[RED_G][RED_Q];
+  __shared__ float bpart[RED_G][RED_Q];
   const agn_wgrad_desc& d = b.d[blockIdx.y];
   const int nsplit = d.nsplit;
   const int nKb = (d.k + DW_BLK - 1) / DW_BLK, nMb = (d.m + DW_BLK - 1) / DW_BLK;
   const int kpad = nKb * DW_BLK, mpad = nMb * DW_BLK;
   const size_t slab = (size_t)mpad * kpad;
   const int kq = kpad / 4;
-  const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int qidx = blockIdx.x * 64 + t;  // column quad over [mpad][kpad / 4]
+  const int t = threadIdx.x % RED_Q, g = threadIdx.x / RED_Q;
+  const int qidx = blockIdx.x * RED_Q + t;  // column quad over [mpad][kpad / 4]
   const bool in_slab = qidx < mpad * kq;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (in_slab) {
     const float* p = d.dw_partial + (size_t)qidx * 4;
-    for (int sp = g; sp < nsplit; sp += RED_G) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(p + sp * slab);
+    // 4 splits' loads in flight per step, added in split order (the same sums)
+    int sp = g;
+    for (; sp + 3 * RED_G < nsplit; sp += 4 * RED_G) {
+      f32x4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4*>(p + (size_t)(sp + j * RED_G) * slab);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[0] += v[j][0]; s[1] += v[j][1]; s[2] += v[j][2]; s[3] += v[j][3];
+      }
+    }
+    for (; sp < nsplit; sp += RED_G) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(p + (size_t)sp * slab);
       s[0] += v[0]; s[1] += v[1]; s[2] += v[2]; s[3] += v[3];
     }
   }
   part[g][t] = s;
-  // bias: block 0.. covers the first 64 bias entries per block
-  const int bi = blockIdx.x * 64 + t;
+  // bias: block b covers bias entries RED_Q b .. RED_Q b + RED_Q - 1
+  const int bi = blockIdx.x * RED_Q + t;
   float bs = 0.f;
   if (d.db && bi < d.m)
     for (int sp = g; sp < nsplit; sp += RED_G) bs += d.db_partial[(size_t)sp * mpad + bi];
@@ -444,7 +458,7 @@ int agn_wgrad(const agn_wgrad_batch* b, int dtype, int nsplit, void* stream) {
   else if (dtype == AGN_F32) AGN_WG(float);
   else return AGN_E_DTYPE;
 #undef AGN_WG
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, st, bb);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + RED_Q - 1) / RED_Q, bb.n), dim3(RED_Q * RED_G), 0, st, bb);
   return launch_status();
 }
 
@@ -458,7 +472,7 @@ int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream) {
     const int mpad = ((bb.d[i].m + DW_BLK - 1) / DW_BLK) * DW_BLK;
     maxq = mpad * kpad / 4 > maxq ? mpad * kpad / 4 : maxq;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + 63) / 64, bb.n), dim3(64 * RED_G), 0, (hipStream_t)stream, bb);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((maxq + RED_Q - 1) / RED_Q, bb.n), dim3(RED_Q * RED_G), 0, (hipStream_t)stream, bb);
   return launch_status();
 }
 
