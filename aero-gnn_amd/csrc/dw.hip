@@ -343,7 +343,15 @@ __global__ void colsum_stage1(const float* __restrict__ p, int nw, int n, int ch
   const int r0 = blockIdx.y * chunk, r1 = min(nw, r0 + chunk);
   if (c >= n) return;
   float s = 0.f;
-  for (int r = r0; r < r1; ++r) s += p[(size_t)r * n + c];
+  int r = r0;
+  for (; r + 3 < r1; r += 4) {  // 4 loads in flight, added in row order
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = p[(size_t)(r + j) * n + c];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[j];
+  }
+  for (; r < r1; ++r) s += p[(size_t)r * n + c];
   part[(size_t)blockIdx.y * n + c] = s;
 }
 
@@ -355,8 +363,17 @@ __global__ __launch_bounds__(64 * RED_G) void colsum_stage2(const float* __restr
   const int t = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + t;
   float s = 0.f;
-  if (c < n)
-    for (int r = g; r < nc; r += RED_G) s += part[(size_t)r * n + c];
+  if (c < n) {
+    int r = g;
+    for (; r + 3 * RED_G < nc; r += 4 * RED_G) {  // 4 loads in flight, added in chunk order
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = part[(size_t)(r + j * RED_G) * n + c];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[j];
+    }
+    for (; r < nc; r += RED_G) s += part[(size_t)r * n + c];
+  }
   red[g][t] = s;
   __syncthreads();
   if (g == 0 && c < n) {
