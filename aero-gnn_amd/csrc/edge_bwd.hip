@@ -795,15 +795,26 @@ AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k
 }
 
 // receivers the in-kernel walk does not finish (edges spanning a round boundary: the walk left
-// partial sums there) and empty ones, after the fused kernel: segment_sum_kernel's thread layout
-// and summation order (16 threads per receiver, 8 features each)
+// partial sums there) and empty ones, after the fused kernel: segment_sum_kernel's summation
+// order (16 threads per receiver, 8 features each). A block checks 256 receivers (one per thread),
+// lists the few that need it (about one in twenty at C3's level 0) and sums those 16 at a time:
+// the check alone used to take 16 threads per receiver (62 us per C3 launch)
 __global__ __launch_bounds__(256) void dpd_cross_kernel(int nodes, const int32_t* __restrict__ ptr,
                                                         const bf16* __restrict__ g0, bf16* __restrict__ dpd) {
+  __shared__ int list[256];
+  __shared__ int cnt;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  {
+    const int n = blockIdx.x * 256 + threadIdx.x;
+    if (n < nodes) {
+      const int beg = ptr[n], end = ptr[n + 1];
+      if (!(end > beg && beg / ROUND_ROWS == (end - 1) / ROUND_ROWS)) list[atomicAdd(&cnt, 1)] = n;
+    }
+  }
+  __syncthreads();
+  const int total = cnt;
   const int sub = threadIdx.x & 15;
-  const int n = blockIdx.x * 16 + (threadIdx.x >> 4);
-  if (n >= nodes) return;
-  const int beg = ptr[n], end = ptr[n + 1];
-  if (end > beg && beg / ROUND_ROWS == (end - 1) / ROUND_ROWS) return;  // summed in the fused kernel
   const int f0 = 8 * sub;
   auto ld8 = [&](float (&o)[8], int row) {
     const u32x4 x = *reinterpret_cast<const u32x4*>(g0 + (size_t)row * H + f0);
@@ -813,25 +824,29 @@ __global__ __launch_bounds__(256) void dpd_cross_kernel(int nodes, const int32_t
       o[2 * i + 1] = hi_bf16(x[i]);
     }
   };
-  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int j = beg;
-  for (; j + 1 < end; j += 2) {
-    float x[8], y[8];
-    ld8(x, j);
-    ld8(y, j + 1);
+  for (int li = threadIdx.x >> 4; li < total; li += 16) {
+    const int n = list[li];
+    const int beg = ptr[n], end = ptr[n + 1];
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int j = beg;
+    for (; j + 1 < end; j += 2) {
+      float x[8], y[8];
+      ld8(x, j);
+      ld8(y, j + 1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
+      for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
+    }
+    if (j < end) {
+      float x[8];
+      ld8(x, j);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += x[i];
+    }
+    u32x4 w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = pack2(s[2 * i], s[2 * i + 1]);
+    *reinterpret_cast<u32x4*>(dpd + (size_t)n * H + f0) = w;
   }
-  if (j < end) {
-    float x[8];
-    ld8(x, j);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] += x[i];
-  }
-  u32x4 w;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = pack2(s[2 * i], s[2 * i + 1]);
-  *reinterpret_cast<u32x4*>(dpd + (size_t)n * H + f0) = w;
 }
 
 // ------------------------------------------------------------------------------ dW wave
@@ -1079,7 +1094,7 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
   if (a->dpd) {
     const int st = launch_status();
     if (st) return st;
-    hipLaunchKernelGGL(dpd_cross_kernel, dim3((a->nodes + 15) / 16), dim3(256), 0, (hipStream_t)stream, a->nodes,
+    hipLaunchKernelGGL(dpd_cross_kernel, dim3((a->nodes + 255) / 256), dim3(256), 0, (hipStream_t)stream, a->nodes,
                        a->rowptr, (const bf16*)a->g0, (bf16*)a->dpd);
   }
   return launch_status();
