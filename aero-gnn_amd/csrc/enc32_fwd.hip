@@ -47,17 +47,17 @@ AGN_DEV void gemm_k8(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const uint4* w, 
 
 struct Walk {
   int first, end, step;
-  AGN_DEV Walk(int ntiles, int w) {
+  AGN_DEV Walk(int ntiles, int w, int nw = NW) {
     if (gridDim.x >= 8 && (gridDim.x & 7) == 0) {
       const int g = blockIdx.x & 7, bi = blockIdx.x >> 3, nb = gridDim.x >> 3;
       const int per = (ntiles + 7) / 8;
-      first = g * per + bi * NW + w;
+      first = g * per + bi * nw + w;
       end = min(ntiles, (g + 1) * per);
-      step = nb * NW;
+      step = nb * nw;
     } else {
-      first = blockIdx.x * NW + w;
+      first = blockIdx.x * nw + w;
       end = ntiles;
-      step = gridDim.x * NW;
+      step = gridDim.x * nw;
     }
   }
 };
@@ -192,17 +192,19 @@ __global__ __launch_bounds__(64 * NW) void enc32_fwd_kernel(const agn_mlp_fwd_ar
 }
 
 // The decoder (mlp.py MLP on H-wide rows to <= 32 outputs, no LayerNorm; models/bsms_mgn.py
-// decoder) at inference, bitwise the general kernel's narrow-output mode (mlp.hip M_NOUT: the last
-// Linear computes output tile 0 only, its bias masked to out_dim): weights resident, 16 waves per CU.
+// decoder), bitwise the general kernel's narrow-output mode (mlp.hip M_NOUT: the last Linear
+// computes output tile 0 only, its bias masked to out_dim), training saves included: weights
+// resident, 16 waves per CU (12 with the saves, which spill at 128 registers).
 template <int NLIN> struct DecSmem {
   uint4 w[NLIN][LW];      // the last image holds output tile 0 only (its first NU * 64 units)
   float pv[NLIN][H];
 };
 static_assert(sizeof(DecSmem<4>) <= 160 * 1024, "LDS budget");
 
-template <int NLIN>
-__global__ __launch_bounds__(64 * NW) void dec32_fwd_kernel(const agn_mlp_fwd_args a) {
-  constexpr int NTHR = 64 * NW;
+// DNW waves per CU: 16 (<= 128 registers) at inference, 12 (<= 168) with the training saves
+template <int NLIN, bool SAVES, int DNW>
+__global__ __launch_bounds__(64 * DNW) void dec32_fwd_kernel(const agn_mlp_fwd_args a) {
+  constexpr int NTHR = 64 * DNW;
   __shared__ DecSmem<NLIN> sm;
   for (int l = 0; l < NLIN; ++l) {
     const uint4* wl = reinterpret_cast<const uint4*>(a.wpk[l]);
@@ -217,7 +219,7 @@ __global__ __launch_bounds__(64 * NW) void dec32_fwd_kernel(const agn_mlp_fwd_ar
   const int lane0 = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntiles = (a.rows + 31) / 32;
-  const Walk walk(ntiles, w);
+  const Walk walk(ntiles, w, DNW);
   const agn_seg& sx = a.seg[0];
   const bf16* X = reinterpret_cast<const bf16*>(sx.ptr);
   for (int tile = walk.first; tile < walk.end; tile += walk.step) {
@@ -241,6 +243,13 @@ __global__ __launch_bounds__(64 * NW) void dec32_fwd_kernel(const agn_mlp_fwd_ar
     for (int l = 1; l < NLIN; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
+      if constexpr (SAVES) {
+        if (a.act[l - 1]) {
+          if (a.tiled) b.store_tiled(reinterpret_cast<bf16*>(a.act[l - 1]), row, h, valid);
+          else b.store(reinterpret_cast<bf16*>(a.act[l - 1]) + (size_t)row * H, h, valid);
+        }
+        if (a.mask[l - 1]) store_relu_mask<bf16, NR>(a.mask[l - 1], b, tile, lane);
+      }
 #pragma unroll
       for (int q = 0; q < 4 * NT; ++q) {
         const f32x4 x = *reinterpret_cast<const f32x4*>(&sm.pv[l][8 * q + 4 * h]);
@@ -329,21 +338,30 @@ bool dec32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc) {
     return false;
   const agn_seg& sx = a->seg[0];
   if (sx.kind != AGN_SEG_PLAIN || sx.k != H || sx.ld % 8 || !sx.ptr || !al16(sx.ptr)) return false;
-  // inference only: with the training saves this kernel spills at 128 registers and measured slower
-  // than the general kernel (the decoder is one launch per step either way)
-  for (int l = 0; l < AGN_MAX_LIN; ++l)
-    if (a->pre[l] || a->act[l] || a->mask[l]) return false;
+  // training saves: relu outputs and their mask bits (no LayerNorm here, so no hpre / stats)
+  bool saves = false;
+  for (int l = 0; l < AGN_MAX_LIN; ++l) {
+    if (a->pre[l] || (l >= a->nlin - 1 && (a->act[l] || a->mask[l]))) return false;
+    saves = saves || a->act[l] || a->mask[l];
+    if (!al16(a->act[l])) return false;
+  }
   if (a->hpre || a->stats) return false;
   for (int l = 0; l < a->nlin; ++l)
     if (!a->wpk[l] || !al16(a->wpk[l])) return false;
+  const int dnw = saves ? 12 : 16;
   const int tiles = (a->rows + 31) / 32;
-  const int need = (tiles + NW - 1) / NW;
+  const int need = (tiles + dnw - 1) / dnw;
   const int cus = cu_count();
   const int nblk = need >= cus ? cus : ((need + 7) / 8 * 8 < 8 ? 8 : (need + 7) / 8 * 8);
-  const dim3 g(nblk), blk(64 * NW);
+  const dim3 g(nblk);
   hipStream_t st = (hipStream_t)stream;
-  if (a->nlin == 4) hipLaunchKernelGGL((dec32_fwd_kernel<4>), g, blk, 0, st, *a);
-  else hipLaunchKernelGGL((dec32_fwd_kernel<3>), g, blk, 0, st, *a);
+  if (saves) {
+    if (a->nlin == 4) hipLaunchKernelGGL((dec32_fwd_kernel<4, true, 12>), g, dim3(64 * 12), 0, st, *a);
+    else hipLaunchKernelGGL((dec32_fwd_kernel<3, true, 12>), g, dim3(64 * 12), 0, st, *a);
+  } else {
+    if (a->nlin == 4) hipLaunchKernelGGL((dec32_fwd_kernel<4, false, 16>), g, dim3(64 * 16), 0, st, *a);
+    else hipLaunchKernelGGL((dec32_fwd_kernel<3, false, 16>), g, dim3(64 * 16), 0, st, *a);
+  }
   ++g_dec_launches;
   const hipError_t e = hipGetLastError();
   *rc = e == hipSuccess ? 0 : (int)e;
