@@ -318,18 +318,20 @@ __global__ __launch_bounds__(256) void gather_rows4_kernel(int rows, const int32
   const int g = blockIdx.x * (256 / SEG_TPR) + threadIdx.x / SEG_TPR;
   using A_t = acc_of<T>;
   A_t x[GR_RPG][8], y[GR_RPG][8];
-  int s[GR_RPG];
+  int s[GR_RPG], cnt[GR_RPG];
 #pragma unroll
   for (int i = 0; i < GR_RPG; ++i) {
     const int r = g + i * ng;
     s[i] = r < rows ? (idx ? idx[r] : r) : -1;
   }
+  // the rows, the addends and the group counts all issued before the first use
 #pragma unroll
   for (int i = 0; i < GR_RPG; ++i) {
     const int r = g + i * ng;
     if (s[i] >= 0) {
       load8(x[i], src + (size_t)s[i] * src_ld, f0, K, true);
       if (add) load8(y[i], add + (size_t)r * add_ld, f0, K, true);
+      if (cnt_ptr) cnt[i] = cnt_ptr[s[i] + 1] - cnt_ptr[s[i]];
     }
   }
 #pragma unroll
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(256) void gather_rows4_kernel(int rows, const int32
     const int r = g + i * ng;
     if (s[i] < 0) continue;
     if (cnt_ptr) {
-      const A_t div = (A_t)max(cnt_ptr[s[i] + 1] - cnt_ptr[s[i]], 1);
+      const A_t div = (A_t)max(cnt[i], 1);
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[i][e] /= div;
     }
