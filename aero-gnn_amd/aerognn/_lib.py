@@ -239,6 +239,7 @@ def lib():
             "agn_debug_enc32_launches": (C.c_long, []),
             "agn_debug_dec32_launches": (C.c_long, []),
             "agn_debug_node32_bwd_launches": (C.c_long, []),
+            "agn_debug_dec32_bwd_launches": (C.c_long, []),
             "agn_edge_backward_blocks": (i32, [i32]),
             "agn_edge_backward": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_fault_status": (i32, [C.POINTER(i32), i32]),

@@ -1287,6 +1287,7 @@ bool node32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);  // node3
 bool enc32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
 bool dec32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
 bool node32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc, int* ln_rows);  // node32_bwd.hip
+bool dec32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc);                  // node32_bwd.hip
 }
 
 extern "C" {
@@ -1407,6 +1408,13 @@ int agn_mlp_backward(const agn_mlp_bwd_args* a, void* stream) {
     int rc = 0, lr = 0;
     if (agn::node32_bwd_try(a, stream, &rc, &lr)) {
       am->ln_rows = lr;
+      return rc;
+    }
+  }
+  if (g_opt_resident && mode == M_NOUT) {  // the decoder from H-wide rows: resident weights
+    int rc = 0;
+    if (agn::dec32_bwd_try(a, stream, &rc)) {
+      am->ln_rows = (int)agn_mlp_bwd_nwaves(a->rows);
       return rc;
     }
   }

@@ -120,6 +120,11 @@ __global__ __launch_bounds__(64 * NW) void node32_bwd_kernel(const agn_mlp_bwd_a
     const int rr = valid ? row : a.rows - 1;
     float A[NR];
     load_g(A, G, rr, valid, h);
+    // every layer's ReLU mask bits, loaded before the tile's first store (vmcnt retires in order:
+    // a load issued after the gpre stores would wait for them)
+    uint32_t mks[3][mask_dwords<NR>()];
+#pragma unroll
+    for (int l = 0; l < 3; ++l) load_relu_mask<NR>(mks[l], a.mask[l], tile, lane);
     {
       // ---- LayerNorm backward (mlp_bwd_kernel: hpre and gamma read per 4-feature chunk, twice)
       const float mean = a.stats[2 * (size_t)rr], rstd = a.stats[2 * (size_t)rr + 1];
@@ -189,10 +194,8 @@ __global__ __launch_bounds__(64 * NW) void node32_bwd_kernel(const agn_mlp_bwd_a
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) A[16 * t + r] = acc[t][r];
-      uint32_t mk[mask_dwords<NR>()];
-      load_relu_mask<NR>(mk, a.mask[l - 1], tile, lane);
 #pragma unroll
-      for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, A[i]);
+      for (int i = 0; i < NR; ++i) A[i] = mask_sel(mks[l - 1], i, A[i]);
     }
     if (a.gpre[0]) {
       if (a.gpre_tiled & 1) store_row_tiled<bf16, NR>(reinterpret_cast<bf16*>(a.gpre[0]), A, row, h, valid);
@@ -239,6 +242,135 @@ __global__ __launch_bounds__(256) void node32_lnp_kernel(const float* __restrict
   out[i] = s;
 }
 
+// ------------------------------------------------------------------------- decoder backward
+// The decoder MLP (H-wide rows -> out_dim <= 32 outputs, no LayerNorm, NLIN = 3 or 4 Linears;
+// models/bsms_mgn.py decoder): bitwise mlp_bwd_kernel<bf16, 4, M_NOUT> on the same operands (the
+// narrow g row loaded as its load_grad, the same MFMA sequence per accumulator, the same masked
+// stores). Every W^T image stays resident (104 KB at most); 8 waves per CU stream 32-row tiles.
+constexpr int LWL = NT * 2 * 64;  // the last layer's W^T: 4 output tiles x <= 2 k-units
+struct DSmem {
+  uint4 w0t[LW];
+  uint4 wh[2][LW];
+  uint4 wl[LWL];
+};
+static_assert(sizeof(DSmem) <= 160 * 1024, "LDS budget");
+
+AGN_DEV void store_narrow(bf16* rowp, int k, const float (&v)[NR], int h, bool valid) {
+  if (!valid) return;
+#pragma unroll
+  for (int q = 0; q < NR / 4; ++q)
+    store4_masked(rowp, 8 * q + 4 * h, k, false, f32x4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]});
+}
+
+template <int NLIN>
+__global__ __launch_bounds__(64 * NW) void dec32_bwd_kernel(const agn_mlp_bwd_args a) {
+  constexpr int NTHR = 64 * NW;
+  __shared__ DSmem sm;
+  const int M = a.out_dim;
+  const int kul = (M + 15) / 16;
+  {
+    const uint4* w0 = reinterpret_cast<const uint4*>(a.wtpk[0]);
+    for (int i = threadIdx.x; i < LW; i += NTHR) sm.w0t[i] = w0[i];
+#pragma unroll
+    for (int l = 1; l + 1 < NLIN; ++l) {
+      const uint4* wg = reinterpret_cast<const uint4*>(a.wtpk[l]);
+      for (int i = threadIdx.x; i < LW; i += NTHR) sm.wh[l - 1][i] = wg[i];
+    }
+    const uint4* wg = reinterpret_cast<const uint4*>(a.wtpk[NLIN - 1]);
+    for (int i = threadIdx.x; i < NT * kul * 64; i += NTHR) sm.wl[i] = wg[i];
+  }
+  __syncthreads();
+  const int lane0 = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntiles = (a.rows + 31) / 32;
+  const Walk walk(ntiles, w);
+  const bf16* G = reinterpret_cast<const bf16*>(a.g);
+  // a tile's loads (the narrow g row, every layer's ReLU mask bits) are issued one tile ahead,
+  // before the current tile's stores: vmcnt retires in order, so a load issued after a tile's
+  // gpre / dx stores would wait for those stores to complete
+  constexpr int ND = mask_dwords<NR>();
+  f32x4 pg[4];
+  uint32_t pm[NLIN - 1][ND];
+  auto prefetch = [&](int t) {
+    const int c = lane0 & 31, h = lane0 >> 5;
+    const int r = min(t * 32 + c, a.rows - 1);
+    const bf16* g1 = G + (size_t)r * M;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pg[q] = load4_masked(g1, 8 * q + 4 * h, M, false);
+#pragma unroll
+    for (int l = 0; l + 1 < NLIN; ++l) load_relu_mask<NR>(pm[l], a.mask[l], t, lane0);
+  };
+  if (walk.first < walk.end) prefetch(walk.first);
+  for (int tile = walk.first; tile < walk.end; tile += walk.step) {
+    cbarrier();
+    const int lane = opaque_v(lane0);
+    const int c = lane & 31, h = lane >> 5;
+    const int row = tile * 32 + c;
+    const bool valid = row < a.rows;
+    float A[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) A[i] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) A[4 * q + e] = valid ? pg[q][e] : 0.f;
+    uint32_t mks[NLIN - 1][ND];
+#pragma unroll
+    for (int l = 0; l + 1 < NLIN; ++l)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) mks[l][d] = pm[l][d];
+    if (tile + walk.step < walk.end) prefetch(tile + walk.step);
+    f32x16 acc[NT];
+    BOp<bf16, NR> b;
+    // ---- the last Linear (out_dim outputs): its G rows, then W^T over kul k-units
+    if (a.gpre[NLIN - 1]) store_narrow(reinterpret_cast<bf16*>(a.gpre[NLIN - 1]) + (size_t)row * M, M, A, h, valid);
+    b.set(A);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+    for (int u = 0; u < kul; ++u)
+#pragma unroll
+      for (int ot = 0; ot < NT; ++ot) b.mfma(acc[ot], sm.wl[(ot * kul + u) * 64 + lane], u);
+#pragma unroll
+    for (int l = NLIN - 1; l >= 1; --l) {
+      cbarrier();
+      if (l < NLIN - 1) {  // a hidden Linear: H -> H
+        if (a.gpre[l]) {
+          if ((a.gpre_tiled >> l) & 1) store_row_tiled<bf16, NR>(reinterpret_cast<bf16*>(a.gpre[l]), A, row, h, valid);
+          else store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.gpre[l]) + (size_t)row * H, A, h, valid);
+        }
+        b.set(A);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+        gemm_l(acc, b, sm.wh[l - 1], 0, lane);
+        cbarrier();
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) A[16 * t + r] = acc[t][r];
+#pragma unroll
+      for (int i = 0; i < NR; ++i) A[i] = mask_sel(mks[l - 1], i, A[i]);
+    }
+    if (a.gpre[0]) {
+      if (a.gpre_tiled & 1) store_row_tiled<bf16, NR>(reinterpret_cast<bf16*>(a.gpre[0]), A, row, h, valid);
+      else store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.gpre[0]) + (size_t)row * H, A, h, valid);
+    }
+    if (a.din[0]) {
+      b.set(A);
+      cbarrier();
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
+      gemm_l(acc, b, sm.w0t, 0, lane);
+      float v[NR];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[16 * t + r] = acc[t][r];
+      store_row_w<bf16, NR>(reinterpret_cast<bf16*>(a.din[0]) + (size_t)row * H, v, h, valid);
+    }
+  }
+}
+
 int g_cus = 0;
 int cu_count() {
   if (g_cus == 0) {
@@ -256,10 +388,18 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 float* g_lnt = nullptr;
 size_t g_lnt_cap = 0;
 long g_launches = 0;
+long g_dec_launches = 0;
+
+int grid_for(int ntiles) {
+  const int need_blocks = (ntiles + NW - 1) / NW;
+  const int cus = cu_count();
+  return need_blocks >= cus ? cus : ((need_blocks + 7) / 8 * 8 < 8 ? 8 : (need_blocks + 7) / 8 * 8);
+}
 
 }  // namespace
 
 extern "C" long agn_debug_node32_bwd_launches(void) { return g_launches; }
+extern "C" long agn_debug_dec32_bwd_launches(void) { return g_dec_launches; }
 
 namespace agn {
 // agn_mlp_backward (mlp.hip) hands over the processor-layer node MLP backward this kernel covers:
@@ -296,15 +436,35 @@ bool node32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc, int* ln_ro
       g_lnt_cap = need;
     }
   }
-  const int need_blocks = (ntiles + NW - 1) / NW;
-  const int cus = cu_count();
-  const int grid = need_blocks >= cus ? cus : ((need_blocks + 7) / 8 * 8 < 8 ? 8 : (need_blocks + 7) / 8 * 8);
+  const int grid = grid_for(ntiles);
   hipLaunchKernelGGL(node32_bwd_kernel, dim3(grid), dim3(64 * NW), 0, st, *a, g_lnt);
   if (a->ln_partial)
     hipLaunchKernelGGL(node32_lnp_kernel, dim3((nblk * 2 * H + 255) / 256), dim3(256), 0, st, g_lnt, ntiles, nblk,
                        a->ln_partial);
   ++g_launches;
   *ln_rows = nblk;
+  const hipError_t e = hipGetLastError();
+  *rc = e == hipSuccess ? 0 : (int)e;
+  return true;
+}
+
+// the decoder's backward (dec32_bwd_kernel); false (nothing launched) for any other call
+bool dec32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc) {
+  if (a->dtype != AGN_BF16 || a->hidden != H || (a->nlin != 3 && a->nlin != 4) || a->out_dim < 1 ||
+      a->out_dim > 32 || a->in_dim != H || a->use_ln || a->act_fn != AGN_ACT_RELU || a->din_nseg != 1 ||
+      a->din_k[0] != H || a->din_resid[0] || a->rows < 64 * 1024 || a->rows >= (1 << 26))
+    return false;
+  if (!a->g || a->g2 || a->gidx || ((a->gpre_tiled >> (a->nlin - 1)) & 1)) return false;
+  for (int l = 0; l + 1 < a->nlin; ++l)
+    if (!a->mask[l]) return false;
+  for (int l = 0; l < a->nlin; ++l)
+    if (!a->wtpk[l] || !al16(a->wtpk[l]) || !al16(a->gpre[l])) return false;
+  if (!al16(a->din[0])) return false;
+  const int ntiles = (a->rows + 31) / 32;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->nlin == 4) hipLaunchKernelGGL(dec32_bwd_kernel<4>, dim3(grid_for(ntiles)), dim3(64 * NW), 0, st, *a);
+  else hipLaunchKernelGGL(dec32_bwd_kernel<3>, dim3(grid_for(ntiles)), dim3(64 * NW), 0, st, *a);
+  ++g_dec_launches;
   const hipError_t e = hipGetLastError();
   *rc = e == hipSuccess ? 0 : (int)e;
   return true;

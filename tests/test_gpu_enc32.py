@@ -122,3 +122,54 @@ def test_dec32_bitwise_general(rows, out_dim, nlin, saves):
     assert torch.equal(o1, o0)
     for a, b in zip(s1, s0):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows,out_dim,nlin,rowmajor", [(70000, 3, 4, ()), (65537, 4, 3, (0,)), (100001, 32, 4, (1,))])
+def test_dec32_backward_bitwise_general(rows, out_dim, nlin, rowmajor):
+    """The resident decoder backward (csrc/node32_bwd.hip dec32_bwd_kernel, picked inside
+    agn_mlp_backward) against the general kernel's narrow-output mode (AGN_OPT_RESIDENT = 0) on the
+    forward's own saves: every pre-activation gradient (tiled and row-major) and dx, bitwise; a
+    partial last tile included."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.core import Pack
+    from aerognn.functions import ChainSpec, _alloc_saves, _alloc_gpre
+    g = torch.Generator(device="cpu").manual_seed(71)
+    ws = [(torch.randn(H, H, generator=g) * H ** -0.5).to(DEV) for _ in range(nlin - 1)] + \
+         [(torch.randn(out_dim, H, generator=g) * H ** -0.5).to(DEV)]
+    bs = [(torch.randn(H, generator=g) * 0.1).to(DEV) for _ in range(nlin - 1)] + \
+         [(torch.randn(out_dim, generator=g) * 0.1).to(DEV)]
+    pack = Pack()
+    spec = ChainSpec(list(zip(ws, bs)), None, H, pack, "d")
+    pack.update(torch.bfloat16, torch.device(DEV))
+    x = torch.randn(rows, H, generator=g).to(torch.bfloat16).to(DEV)
+    gy = torch.randn(rows, out_dim, generator=g).to(torch.bfloat16).to(DEV)
+    out = torch.empty(rows, out_dim, dtype=torch.bfloat16, device=DEV)
+    acts, _, _ = _alloc_saves(spec, rows, torch.bfloat16, x.device, True)
+    core.mlp_forward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=nlin, out_dim=out_dim,
+                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None)], wpk=spec.wpk(),
+                     bias=spec.biases(), out=out, acts=acts)
+    lib = L.lib()
+    res = []
+    for resident in (False, True):
+        n0 = lib.agn_debug_dec32_bwd_launches()
+        old = lib.agn_set_option(L.OPT_RESIDENT, int(resident))
+        try:
+            gpre = _alloc_gpre(spec, rows, torch.bfloat16, x.device, rowmajor)
+            for t in gpre:
+                t.zero_()
+            dx = torch.full_like(x, float("nan"))
+            nb = core.mlp_backward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=nlin, out_dim=out_dim,
+                                   in_dim=H, wtpk=spec.wtpk(), acts=acts, g=gy, gpre=gpre,
+                                   din=[(H, dx, False)])
+            torch.cuda.synchronize()
+        finally:
+            lib.agn_set_option(L.OPT_RESIDENT, old)
+        assert lib.agn_debug_dec32_bwd_launches() - n0 == int(resident)
+        res.append((nb, gpre, dx))
+    (nb0, gp0, dx0), (nb1, gp1, dx1) = res
+    assert nb0 == nb1
+    assert bool(torch.isfinite(dx0.float()).all())
+    assert torch.equal(dx1, dx0)
+    for a, b in zip(gp1, gp0):
+        assert torch.equal(a, b)
