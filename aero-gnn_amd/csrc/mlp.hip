@@ -1039,6 +1039,10 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
     BOp<T, NR> b;
     for (int l = a.nlin - 1; l >= 0; --l) {
       cbarrier();
+      // AGN_RELU_MASK sign bits (res_bwd_ok: always given), issued before this layer's gpre store:
+      // vmcnt retires in order, so a load issued after the store would wait for it to complete
+      uint32_t mk[mask_dwords<NR>()];
+      if (l > 0) load_relu_mask<NR>(mk, a.mask[l - 1], tile, lane);
       if (a.gpre[l]) {
         if ((a.gpre_tiled >> l) & 1) store_row_tiled<T, NR>(reinterpret_cast<T*>(a.gpre[l]), A, row, h, valid);
         else store_row_w<T, NR>(reinterpret_cast<T*>(a.gpre[l]) + (size_t)row * H, A, h, valid);
@@ -1047,9 +1051,6 @@ __global__ __launch_bounds__(RES_BLOCK, 2) void mlp_bwd_res_kernel(const agn_mlp
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = f32x16{};
       if (l > 0) {
-        // AGN_RELU_MASK sign bits (res_bwd_ok: always given), issued before the MFMAs
-        uint32_t mk[mask_dwords<NR>()];
-        load_relu_mask<NR>(mk, a.mask[l - 1], tile, lane);
         gemm<T, NT, NR, true>(acc, b, NUH, wres + l * LAYER, NUH, NT, lane);
 #pragma unroll
         for (int i = 0; i < NR; ++i) A[i] = mask_sel(mk, i, acc[i / 16][i % 16]);
