@@ -256,12 +256,17 @@ __global__ __launch_bounds__(64 * NW) void node32_fwd_kernel(const agn_mlp_fwd_a
     for (int l = 1; l < NLIN; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
-      if constexpr (SAVES) {
+      auto save = [&]() {
         if (a.act[l - 1]) {
           if (a.tiled) b.store_tiled(reinterpret_cast<bf16*>(a.act[l - 1]), row_b, hb, valid_b);
           else b.store(reinterpret_cast<bf16*>(a.act[l - 1]) + (size_t)row_b * H, hb, valid_b);
         }
         if (a.mask[l - 1]) store_relu_mask<bf16, NR>(a.mask[l - 1], b, tile, lane_b);
+      };
+      // the layer whose weights stream from L2 (W3) saves its input after the product: vmcnt retires
+      // loads and stores in issue order, so W3 fragments loaded after the saves would wait for them
+      if constexpr (SAVES) {
+        if (l != 3) save();
       }
 #pragma unroll
       for (int q = 0; q < 4 * NT; ++q) {
@@ -271,6 +276,9 @@ __global__ __launch_bounds__(64 * NW) void node32_fwd_kernel(const agn_mlp_fwd_a
       }
       if (l == 3) gemm_k8_g(acc, b, reinterpret_cast<const uint4*>(a.wpk[3]), lane_b);
       else gemm_k8(acc, b, l == 1 ? sm.w1 : sm.w2, NU, 0, lane_b);
+      if constexpr (SAVES) {
+        if (l == 3) save();
+      }
     }
     cbarrier();
     if constexpr (SAVES) {  // the pre-LayerNorm row (the backward's LayerNorm input)
