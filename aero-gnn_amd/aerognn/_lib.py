@@ -18,10 +18,6 @@ MAX_SEG = 3
 F32, BF16, F16, F64 = 0, 1, 2, 3
 SEG_PLAIN, SEG_GATHER, SEG_SUM, SEG_MEAN = 0, 1, 2, 3
 OPT_RESIDENT = 0
-OPT_EDGE_FWD_HALVES = 1
-OPT_EDGE_FWD_WAVES = 2
-OPT_EDGE_FWD32_WAVES = 3
-OPT_EDGE_FWD32_PRIO = 4
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -86,8 +82,8 @@ class WecArgs(C.Structure):
 class EdgeBwdArgs(C.Structure):
     _fields_ = [("rows", i32), ("nblk", i32), ("wpk", vp * 4), ("bias", vp * 4), ("ln_g", vp), ("e", vp),
                 ("proj", vp), ("src", vp), ("dst", vp), ("g", vp), ("g2", vp), ("de", vp), ("g0", vp),
-                ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp), ("dpd", vp),
-                ("rowptr", vp), ("nodes", i32)]
+                ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp),
+                ("a1", vp), ("stats", vp), ("scratch", vp), ("wtpk0", vp)]
 
 
 class EdgeFwdArgs(C.Structure):
@@ -133,7 +129,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
             "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
-            "agn_edge_forward", "agn_edge_forward32", "agn_edge_backward",
+            "agn_edge_forward32",
             "agn_proj_forward", "agn_proj_backward")
 
 
@@ -225,14 +221,13 @@ def lib():
             "agn_scatter_rows": (i32, [i32, i32, i32, vp, vp, i32, vp, i32, vp]),
             "agn_wec_blocks": (i32, [i32]),
             "agn_edge_bwd_blocks": (i32, [i32]),
+            "agn_edge_bwd_scratch_bytes": (C.c_size_t, [i32]),
             "agn_edge_features": (i32, [i32, C.c_int64, i32, vp, vp, i32, vp, vp, vp, vp, vp]),
             "agn_normalize": (i32, [i32, i32, vp, i32, vp, vp, vp, i32, i32, vp]),
             "agn_col_stats_temp_bytes": (C.c_size_t, [i32, i32]),
             "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),
             "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
-            "agn_edge_fwd_blocks": (i32, [i32]),
-            "agn_edge_forward": (i32, [C.POINTER(EdgeFwdArgs), vp]),
             "agn_edge_fwd32_blocks": (i32, [i32]),
             "agn_edge_forward32": (i32, [C.POINTER(EdgeFwdArgs), vp]),
             "agn_debug_node32_launches": (C.c_long, []),
@@ -240,10 +235,9 @@ def lib():
             "agn_debug_dec32_launches": (C.c_long, []),
             "agn_debug_node32_bwd_launches": (C.c_long, []),
             "agn_debug_dec32_bwd_launches": (C.c_long, []),
-            "agn_edge_backward_blocks": (i32, [i32]),
-            "agn_edge_backward": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_fault_status": (i32, [C.POINTER(i32), i32]),
             "agn_fault_status_async": (i32, [vp, vp]),
+            "agn_debug_set_fault": (i32, [i32]),
             "agn_wgrad_reduce": (i32, [C.POINTER(WgradBatch), i32, vp]),
             "agn_proj_forward": (i32, [i32, vp, i32, vp, vp, vp, i32, vp]),
             "agn_proj_backward": (i32, [i32, vp, vp, i32, vp, vp, i32, vp]),
@@ -263,15 +257,6 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = _Lib(L)
-        # A/B measurements: agn_edge_forward's halves per wave and waves per CU
-        # (AGN_OPT_EDGE_FWD_HALVES / _WAVES)
-        for env, key, ok in (("AEROGNN_EDGE_FWD_HALVES", OPT_EDGE_FWD_HALVES, "1 or 2"),
-                             ("AEROGNN_EDGE_FWD_WAVES", OPT_EDGE_FWD_WAVES, "12 or 16"),
-                             ("AEROGNN_EDGE_FWD32_WAVES", OPT_EDGE_FWD32_WAVES, "12 or 16"),
-                             ("AEROGNN_EDGE_FWD32_PRIO", OPT_EDGE_FWD32_PRIO, "0, 1 or 2")):
-            v = os.environ.get(env)
-            if v and L.agn_set_option(key, int(v)) < 0:
-                raise AeroGNNError(f"{env}={v}: {ok}")
     return _lib
 
 

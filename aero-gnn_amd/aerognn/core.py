@@ -301,7 +301,6 @@ def mlp_backward(*, rows, dtype, hidden, nlin, out_dim, in_dim, wtpk, acts, g, g
 # AEROGNN_CHECK_FAULTS=1 (set by the test suite): read the device fault word after every
 # persistent hand-off launch (a device synchronisation each time; never on the timed path).
 CHECK_FAULTS = __import__("os").environ.get("AEROGNN_CHECK_FAULTS", "0") == "1"
-E16_SAVES = None  # parity tests: a list that the 16-row-tile edge forward appends its saves to
 STAMPS = None  # diagnostics: a uint64 device tensor of 2*8*8*16 entries (a -DAGN_EB_STAMPS library)
 
 
@@ -316,97 +315,141 @@ def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
             and nlin == 4 and has_ln and rows >= 64 * 1024)
 
 
-def edge16_ok(dtype, hidden, nlin, has_ln, train):
-    """The 16-row-tile edge chain kernels (csrc/edge16*.hip: agn_edge_forward / agn_edge_backward)
-    apply to bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN). Inference takes the 32-row
-    forward (agn_edge_forward32, edge32_ok) first, the 16-row one with AEROGNN_EDGE32=0
-    (AEROGNN_EDGE16=0 turns this one off too). Training keeps the 32-row pair (agn_edge_forward32,
-    bitwise the resident agn_mlp_forward kernel, + agn_edge_bwd_fused) unless
-    AEROGNN_EDGE16_TRAIN=1: the 16-row fused backward measured slower."""
-    import os
-    if not (os.environ.get("AEROGNN_EDGE16", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
-            and nlin == 4 and has_ln):
-        return False
-    return (not train) or os.environ.get("AEROGNN_EDGE16_TRAIN", "0") == "1"
-
-
 def edge32_ok(dtype, hidden, nlin, has_ln, act=0):
     """agn_edge_forward32 (csrc/edge32_fwd.hip) applies to the bf16 H=128 sum-trick ReLU edge chain
-    (W_e + 3 Linears + LN); AEROGNN_EDGE32=0 turns it off (then inference takes the 16-row forward,
-    training the resident agn_mlp_forward kernel, bitwise the same outputs as this one)."""
+    (W_e + 3 Linears + LN); AEROGNN_EDGE32=0 turns it off (then the resident agn_mlp_forward kernel
+    runs, bitwise the same outputs)."""
     import os
     return (os.environ.get("AEROGNN_EDGE32", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
             and nlin == 4 and has_ln and act == 0)
 
 
-def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, acts=None, hpre=None, stats=None, tag=None,
-                 cost=None, tiles32=False):
-    """agn_edge_forward: out = e + LN(chain(e, P_s[src] + P_d[dst])); acts / hpre / stats are optional
-    row-major saves (parity tests only). tiles32: agn_edge_forward32, the 32-row-tile kernel (no
-    saves; bitwise the resident agn_mlp_forward kernel)."""
+def edge_saves_ok():
+    """The training forward saves a1 and the LayerNorm statistics for the fused backward
+    (agn_edge_forward32 act[0] / stats), which then starts its recompute at Lin1 (DESIGN.md §9,
+    round 6). AEROGNN_EB_SAVED=0: save nothing, recompute h0 from e and the projection rows."""
+    import os
+    return os.environ.get("AEROGNN_EB_SAVED", "1") != "0"
+
+
+def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, a1=None, stats=None, tag=None, cost=None):
+    """agn_edge_forward32: out = e + LN(chain(e, P_s[src] + P_d[dst])) on 32-row tiles (bitwise the
+    resident agn_mlp_forward kernel); a1 (AGN_TILED, tiled_empty) and stats ([rows, 2] fp32) are the
+    fused backward's training saves, both or neither."""
     lib = L.lib()
-    if tiles32 and (acts is not None or hpre is not None or stats is not None):
-        raise L.AeroGNNError("agn_edge_forward32 writes no saves")
     a = L.EdgeFwdArgs()
     a.rows = int(rows)
-    a.nblk = int(lib.agn_edge_fwd32_blocks(int(rows)) if tiles32 else lib.agn_edge_fwd_blocks(int(rows)))
+    a.nblk = int(lib.agn_edge_fwd32_blocks(int(rows)))
     for i in range(4):
         a.wpk[i] = wpk[i]
         a.bias[i] = bias[i]
     a.ln_g, a.ln_b = ln
     a.e, a.proj, a.src, a.dst, a.out = ptr(e), ptr(proj), ptr(src), ptr(dst), ptr(out)
-    for i in range(3):
-        a.act[i] = ptr(acts[i]) if acts is not None else None
-    a.hpre, a.stats = ptr(hpre), ptr(stats)
+    a.act[0] = ptr(a1)
+    a.stats = ptr(stats)
     with timed(tag, cost):
-        if tiles32:
-            check(lib.agn_edge_forward32(C.byref(a), stream()), "edge_forward32")
-        else:
-            check(lib.agn_edge_forward(C.byref(a), stream()), "edge_forward")
+        check(lib.agn_edge_forward32(C.byref(a), stream()), "edge_forward32")
 
 
 # Production-path fault polling (ADVICE r4): every FAULT_POLL_EVERY fused launches an async copy
-# of the device fault words goes to page-locked host memory (agn_fault_status_async, no device
-# synchronisation); a later launch reads it once the copy's event has completed, so a ring
-# timeout raises at most a step or two after it happened instead of leaving wrong dW silently.
+# of the device fault word goes to page-locked host memory (agn_fault_status_async, no device
+# synchronisation); a later launch reads it once the copy's event has completed. At every optimizer
+# step (a global step pre-hook, registered with the first fused launch) fault_checkpoint() raises on a
+# completed copy and enqueues one that covers the launches since the last, so the final <= 15 launches
+# of a run are read too (VERDICT r5 item 8); an atexit hook waits for the last copy. A fault is fatal to
+# the job: under torchrun the raising rank's exit ends the other ranks (they would otherwise wait in
+# the next all-reduce).
 FAULT_POLL_EVERY = 16
-_fault = {"buf": None, "event": None, "n": 0}
+_fault = {"buf": None, "event": None, "n": 0, "dirty": False, "hooked": False}
+
+
+def _fault_read(block):
+    st = _fault
+    ev = st["event"]
+    if ev is None:
+        return
+    if block:
+        ev.synchronize()
+    elif not ev.query():
+        return
+    f = int(st["buf"][0])
+    st["event"] = None
+    if f:
+        raise L.AeroGNNError(f"fused edge backward: device fault word {f:#x} (LDS ring wait timed out; "
+                             "dW of a recent step invalid)")
+
+
+def _fault_enqueue():
+    st = _fault
+    if st["buf"] is None:
+        st["buf"] = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    check(L.lib().agn_fault_status_async(C.c_void_p(st["buf"].data_ptr()), stream()), "fault_status_async")
+    ev = torch.cuda.Event()
+    ev.record()
+    st["event"] = ev
+    st["n"] = 0
+    st["dirty"] = False
+
+
+def fault_checkpoint(block=False):
+    """Step boundary: raise if a completed copy of the fault word is nonzero, then enqueue a copy
+    covering every fused launch so far (if any ran since the last); block=True waits for it and
+    raises on a fault (the end of a run)."""
+    _fault_read(False)
+    if _fault["dirty"]:
+        if _fault["event"] is not None:  # the previous copy first (one buffer)
+            _fault_read(True)
+        _fault_enqueue()
+    if block:
+        _fault_read(True)
+
+
+def _step_pre_hook(_opt, _args, _kwargs):
+    fault_checkpoint()
+
+
+def _exit_check():
+    try:
+        fault_checkpoint(block=True)
+    except L.AeroGNNError as exc:
+        import sys
+        print(f"aerognn: {exc}", file=sys.stderr)
+        raise
 
 
 def _poll_faults():
     st = _fault
-    ev = st["event"]
-    if ev is not None and ev.query():
-        f = int(st["buf"][0]) | int(st["buf"][1])
-        st["event"] = None
-        if f:
-            raise L.AeroGNNError(f"fused edge backward: device fault word {f:#x} (LDS ring wait timed out; "
-                                 "dW of a recent step invalid)")
+    if not st["hooked"]:
+        import atexit
+        torch.optim.optimizer.register_optimizer_step_pre_hook(_step_pre_hook)
+        atexit.register(_exit_check)
+        st["hooked"] = True
+    _fault_read(False)
+    st["dirty"] = True
     st["n"] += 1
     if st["event"] is None and st["n"] >= FAULT_POLL_EVERY:
-        st["n"] = 0
-        if st["buf"] is None:
-            st["buf"] = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-        check(L.lib().agn_fault_status_async(C.c_void_p(st["buf"].data_ptr()), stream()), "fault_status_async")
-        ev = torch.cuda.Event()
-        ev.record()
-        st["event"] = ev
+        _fault_enqueue()
 
 
-def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None, e16=False,
-                   dpd=None, rowptr=None):
-    """agn_edge_backward (e16, the 16-row-tile kernel) or agn_edge_bwd_fused (the 32-row kernel);
-    returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm partials [nblk, 256]
-    fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce). With dpd ([N, 128], the
-    32-row kernel only) and rowptr (the receivers' CSC offsets) it also writes dP_d, bitwise
-    segment_sum(N, 128, rowptr, None, g0)."""
+def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de, g0, tag=None, cost=None,
+                   a1=None, stats=None, scratch=None):
+    """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm
+    partials [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce).
+    a1 / stats: the forward's saves (agn_edge_forward32);
+    then e, proj and src are not read. scratch None: AEROGNN_EB_SCRATCH (default on) decides whether
+    a2 / a3 go through the L2 scratch instead of a second recompute (bitwise the same outputs)."""
+    import os
     lib = L.lib()
-    dev = e.device
+    dev = g2.device
     H = 128
-    nblk = int((lib.agn_edge_backward_blocks if e16 else lib.agn_edge_bwd_blocks)(int(rows)))
+    nblk = int(lib.agn_edge_bwd_blocks(int(rows)))
     dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
     dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
     lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
+    if scratch is None:
+        scratch = os.environ.get("AEROGNN_EB_SCRATCH", "1") != "0"
+    scr = (torch.empty(int(lib.agn_edge_bwd_scratch_bytes(nblk)), dtype=torch.uint8, device=dev)
+           if scratch else None)
     a = L.EdgeBwdArgs()
     a.rows, a.nblk = int(rows), nblk
     for i in range(4):
@@ -417,15 +460,10 @@ def edge_bwd_fused(*, rows, wpk, bias, ln_g, e, proj, src, dst, g, g2, de, g0, t
     a.g, a.g2 = ptr(g), ptr(g2)
     a.de, a.g0, a.dw_partial, a.db_partial, a.ln_partial = ptr(de), ptr(g0), ptr(dwp), ptr(dbp), ptr(lnp)
     a.stamps = ptr(STAMPS)
-    if dpd is not None:
-        if e16 or rowptr is None:
-            raise ValueError("edge_bwd_fused: dpd needs the 32-row kernel and rowptr")
-        a.dpd, a.rowptr, a.nodes = ptr(dpd), ptr(rowptr), int(dpd.shape[0])
+    a.a1, a.stats, a.scratch = ptr(a1), ptr(stats), ptr(scr)
+    a.wtpk0 = wtpk0  # W_e^T packed (ChainSpec.wtpk()[0])
     with timed(tag, cost):
-        if e16:
-            check(lib.agn_edge_backward(C.byref(a), stream()), "edge_backward")
-        else:
-            check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
+        check(lib.agn_edge_bwd_fused(C.byref(a), stream()), "edge_bwd_fused")
     if CHECK_FAULTS:  # tests / debug runs: a bounded ring wait that gave up is an error, not wrong dW
         f = L.fault_status(reset=True)
         if f:
@@ -590,9 +628,11 @@ def mask_bytes(H):
     return 8 * max(1, (H + 63) // 64)
 
 
-def cost_edge_fwd(E, N, H, s, nlin, train):
-    """Minimum HBM bytes / MFMA flops of one fused edge-MLP launch."""
+def cost_edge_fwd(E, N, H, s, nlin, train, a1_saves=False):
+    """Minimum HBM bytes / MFMA flops of one fused edge-MLP launch (SURVEY §8d, DESIGN.md);
+    a1_saves: agn_edge_forward32's training saves for the fused backward (a1 + statistics)."""
     per = 2 * H * s + 8 + ((nlin - 1) * (H * s + mask_bytes(H)) + H * s + 8 if train else 0)
+    per += (H * s + 8) if a1_saves else 0
     return E * per + N * 2 * H * s, 2 * E * H * H * nlin
 
 
@@ -639,9 +679,13 @@ def cost_node_bwd(N, H, s, nlin):
     return N * per, 2 * N * H * (H * (nlin - 1) + 2 * H)
 
 
-def cost_edge_bwd_fused(E, N, H, s):
+def cost_edge_bwd_fused(E, N, H, s, saved=False):
     """agn_edge_bwd_fused: per edge the ids, e, the sender's projection row, g, and de + G0 written
-    (+ the row re-reads of g for de, L2); per receiver its P_d row and dAgg row."""
+    (+ the row re-reads of g for de, L2); per receiver its P_d row and dAgg row. saved: a1 and the
+    statistics instead of e and the projection rows (one Linear fewer recomputed)."""
+    if saved:
+        per = 4 + 8 + H * s * 2 + H * s * 2
+        return E * per + N * H * s, 2 * E * H * H * (3 + 4 + 3)
     per = 8 + H * s * 3 + H * s * 2
     flops = 2 * E * H * H * (4 + 2 + 4 + 3)  # forward 4 + recompute 2 + dX 4 + dW 3 Linears
     return E * per + N * 2 * H * s, flops

@@ -23,7 +23,7 @@ from . import _lib as L
 from ._lib import check, ptr
 from . import core as _core
 from .core import (Pack, WGrad, alg8d_edge, alg8d_node, with_alg, edge_bwd_fused, fused_edge_train_ok, bwd_nblocks,
-                   edge16_ok, edge32_ok, edge_forward,
+                   edge32_ok, edge_saves_ok, edge_forward,
                    cost_edge_bwd_fused,
                    proj_kernel_ok, proj_forward, proj_backward, tiled_empty, relu_mask_empty, colsum_rows, cost_edge_bwd, cost_edge_bwd_cat, cost_edge_fwd,
                    cost_edge_fwd_cat, cost_node_bwd, cost_node_fwd, cost_proj, cost_wec_bwd, cost_wec_fwd, dt_code,
@@ -348,7 +348,10 @@ class LayerSpec:
         self.trick, self.gmp_order, self.aggregation = False, True, "add"
         acts = {torch.nn.ReLU: "relu", torch.nn.SiLU: "silu", torch.nn.GELU: "gelu", torch.nn.Tanh: "tanh"}
         ea, na = acts.get(type(gmp.edge_mlp[1])), acts.get(type(gmp.node_mlp[1]))
-        if ea is None or na is None or (isinstance(gmp.edge_mlp[1], torch.nn.GELU) and gmp.edge_mlp[1].approximate != "none"):
+        # the kernels compute the exact (erf) GELU: a tanh-approximated one on either MLP is refused
+        tanh_gelu = any(isinstance(m[1], torch.nn.GELU) and m[1].approximate != "none"
+                        for m in (gmp.edge_mlp, gmp.node_mlp))
+        if ea is None or na is None or tanh_gelu:
             raise NotImplementedError("aerognn GMP kernels implement ReLU / SiLU / GELU / Tanh MLPs")
         e0, e2, eln = gmp.edge_mlp[0], gmp.edge_mlp[2], gmp.edge_mlp[3]
         n0, n2, nln = gmp.node_mlp[0], gmp.node_mlp[2], gmp.node_mlp[3]
@@ -395,16 +398,18 @@ class GMPFn(torch.autograd.Function):
         es, ns = spec.edge, spec.node
         e_out = torch.empty_like(e)
         x_out = torch.empty_like(x)
-        # fused edge backward: the chain is recomputed there, the forward saves nothing for it
+        # fused edge backward: the chain is recomputed there from the forward's a1 and LayerNorm
+        # statistics (or from e and P); the split path's saves are not needed
         fused = train and spec.trick and fused_edge_train_ok(E, dt, H, es.nlin, es.ln is not None)
-        # the 16-row-tile pair (agn_edge_forward / agn_edge_backward) whenever no split-path saves
-        # are needed: inference, and training with the fused backward
-        e16 = spec.trick and (fused or not train) and edge16_ok(dt, H, es.nlin, es.ln is not None, train)
-        # the 32-row-tile forward (agn_edge_forward32, bitwise the resident agn_mlp_forward kernel the
-        # 32-row fused backward recomputes): inference and the fused training step, unless the
-        # 16-row pair trains or a parity test captures the 16-row kernel's saves
-        e32 = (spec.trick and (fused or not train) and not (train and e16) and _core.E16_SAVES is None
-               and edge32_ok(dt, H, es.nlin, es.ln is not None, es.act) and e.stride(0) == H)
+        # the 32-row-tile forward (agn_edge_forward32, bitwise the resident agn_mlp_forward kernel
+        # the fused backward recomputes): inference and the fused training step
+        e32 = (spec.trick and (fused or not train) and edge32_ok(dt, H, es.nlin, es.ln is not None, es.act)
+               and e.stride(0) == H)
+        # fused training on it: the forward saves a1 and the LayerNorm statistics, and the fused
+        # backward starts its recompute from them (AEROGNN_EB_SAVED=0: it recomputes from e, P)
+        saved = fused and e32 and edge_saves_ok()
+        a1s = tiled_empty(E, H, dt, dev) if saved else None
+        sts = torch.empty(E, 2, dtype=torch.float32, device=dev) if saved else None
         ea, ehp, est = _alloc_saves(es, E, dt, dev, train and not fused)
         na, nhp, nst = _alloc_saves(ns, N, dt, dev, train)
         P = None
@@ -421,23 +426,9 @@ class GMPFn(torch.autograd.Function):
                             tag="proj", cost=with_alg(alg8d_node(N, H, sz), cost_proj(N, H, sz)))
             if e32:
                 edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=level.src,
-                             dst=level.dst, out=e_out, tiles32=True,
+                             dst=level.dst, out=e_out, a1=a1s, stats=sts,
                              tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
-                                                                                                 False)))
-                e16 = False
-            elif e16:
-                # 16-row-tile kernel (csrc/edge16_fwd.hip); the fused backward recomputes it bitwise.
-                # core.E16_SAVES (parity tests only): also save a1..a3, h3 and the LN statistics
-                sv = None
-                if _core.E16_SAVES is not None:
-                    sv = ([torch.empty(E, H, dtype=dt, device=dev) for _ in range(3)],
-                          torch.empty(E, H, dtype=dt, device=dev), torch.empty(E, 2, dtype=torch.float32, device=dev))
-                    _core.E16_SAVES.append((E, e, P, level) + sv)
-                edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=level.src,
-                             dst=level.dst, out=e_out, acts=sv[0] if sv else None, hpre=sv[1] if sv else None,
-                             stats=sv[2] if sv else None,
-                             tag="edge_fwd", cost=with_alg(alg8d_edge(E, N, H, sz), cost_edge_fwd(E, N, H, sz, es.nlin,
-                                                                                                 False)))
+                                                                                                 False, a1_saves=saved)))
             else:
                 mlp_forward(rows=E, dtype=dt, hidden=H, nlin=es.nlin, act_fn=es.act, out_dim=H,
                             segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)],
@@ -471,7 +462,7 @@ class GMPFn(torch.autograd.Function):
                                                                  ns.nlin, train)))
         ctx.spec, ctx.level = spec, level
         ctx.saves = (ea, ehp, est, na, nhp, nst, agg)
-        ctx.fused, ctx.proj, ctx.e16 = fused, (P if fused else None), e16
+        ctx.fused, ctx.proj, ctx.esaves = fused, (P if fused and not saved else None), (a1s, sts)
         ctx.save_for_backward(x, e)
         # an unused e' (the U-Net restores fine edges from the skip, bsms_mgn.py:203) arrives as
         # None instead of a materialised [E,H] zero tensor; the kernels read it as zero
@@ -508,12 +499,11 @@ class GMPFn(torch.autograd.Function):
         if fused:
             # one launch: forward recompute, LayerNorm backward, chain rule, dW1..dW3 / db1..db3
             g0 = torch.empty(E, H, dtype=dt, device=dev)
-            # the 32-row kernel also forms dP_d (the receiver sums of G0) on its dW waves
-            dPd = None if ctx.e16 else torch.empty(N, H, dtype=dt, device=dev)
+            a1s, sts = ctx.esaves
             dW13, db13, part_e, nb_e = edge_bwd_fused(
-                rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=ctx.proj, src=lv.src, dst=lv.dst,
-                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd", e16=ctx.e16, dpd=dPd, rowptr=lv.rowptr,
-                cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True), cost_edge_bwd_fused(E, N, H, sz)))
+                rows=E, wpk=es.wpk(), wtpk0=es.wtpk()[0], bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=ctx.proj, src=lv.src, dst=lv.dst,
+                g=ge, g2=dagg, de=de, g0=g0, tag="edge_bwd", a1=a1s, stats=sts,
+                cost=with_alg(alg8d_edge(E, N, H, sz, bwd=True), cost_edge_bwd_fused(E, N, H, sz, saved=a1s is not None)))
         else:
             nb_e = bwd_nblocks(E)
             part_e = torch.empty(nb_e, 2 * H, dtype=torch.float32, device=dev) if es.ln else None
@@ -536,9 +526,10 @@ class GMPFn(torch.autograd.Function):
         grads_edge = []
         if spec.trick:
             # sum-trick: h0 = e W_e^T + P_s[src] + P_d[dst]: dP by sender / receiver groups
+            # (dP_d formed on the fused kernel's dW waves, round 5, measured slower once the chain
+            # waves got faster: DESIGN.md §9 round 6)
             dPs = segment_sum(N, H, lv.rowptr_src, lv.perm_src, g0, torch.empty(N, H, dtype=dt, device=dev))
-            if not fused or dPd is None:
-                dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
+            dPd = segment_sum(N, H, lv.rowptr, None, g0, torch.empty(N, H, dtype=dt, device=dev))
             if proj_kernel_ok(dx, H):
                 s_el = dx.element_size()
                 proj_backward(N, dPs, dPd, spec.pack["projT"], dx, tag="proj_bwd",

@@ -7,12 +7,17 @@
 //
 // Why a second kernel: the chain is vector-issue-bound on the SIMD, not HBM- or MFMA-bound
 // (DESIGN.md §9 round 5). A v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its
-// 32 cycles, a 16x16x32 for 8 of 16: the 32-row tile halves the MFMA share of the issue budget
-// against edge16_fwd.hip, and the exact MFMA row sum replaces ~190 VALU unpack/add instructions
-// per tile. Against the resident kernel (two waves per SIMD at <= 256 registers, the previous
-// tile's stores deferred in registers) this one runs NW / 4 waves per SIMD: 12 waves at <= 168
-// registers keep the residual operand, 16 waves at <= 128 re-read it in the epilogue; the weight
-// fragments stream two deep instead of a whole k-step ahead.
+// 32 cycles; the exact MFMA row sum replaces ~190 VALU unpack/add instructions per tile. Against the
+// resident kernel (two waves per SIMD at <= 256 registers, the previous tile's stores deferred in
+// registers) this one runs three waves per SIMD at <= 168 registers, keeping the residual
+// operand; the weight fragments stream two deep instead of a whole k-step ahead. (16 waves at
+// <= 128 registers, re-reading the residual, spilled and ran 0.94 -> 1.64 ms per C3 launch;
+// static per-SIMD wave priorities changed nothing: both removed in round 6.)
+//
+// Training saves (SAVE): the first ReLU output a1 in AGN_TILED (the packed operand as it stands, one
+// 1-KB store per unit) and the LayerNorm (mean, rstd). The fused backward (edge_bwd.hip) starts its
+// recompute at Lin1 from them: 264 B per edge written here against e, P_s[src], P_d[dst], W_e and the
+// statistics recomputed there.
 //
 // Persistent: one workgroup per CU, the four packed weight images resident in LDS (128 KB), each
 // wave streaming 32-row tiles in CSC order over an XCD-grouped walk; a tile's node ids are loaded
@@ -34,19 +39,21 @@ constexpr int LAYER = NT * NU * 64;     // packed units (16 B) per weight image
 #define AGN_E32_PF 2
 #endif
 constexpr int PF = AGN_E32_PF;          // weight fragments in flight
+#ifndef AGN_E32_A1
+#define AGN_E32_A1 0  // where the a1 training save is stored (A/B builds: 1 behind Lin1's MFMAs, 2 non-temporal, 3 none)
+#endif
 #ifndef AGN_E32_DIAG
 #define AGN_E32_DIAG 0  // timing diagnostics only (tools/fwd_probe.py): 1 no LayerNorm, 2 no residual, 3 no row sum
 #endif
 
-int g_nw = 12;    // waves per CU (AGN_OPT_EDGE_FWD32_WAVES)
-int g_prio = 0;   // static wave priorities (AGN_OPT_EDGE_FWD32_PRIO)
+constexpr int NW = 12;  // waves per CU (three per SIMD)
 
-template <int NW> struct Smem {
+struct Smem {
   uint4 w[4 * LAYER];   // packed A units [layer][ot][ku][lane] (agn_pack trans = 0 layout, as is)
   float pv[5][H];       // b1, b2, b3, LN gamma, LN beta
   int ids[NW][64];      // per wave: next tile's src (lanes 0-31) / dst (32-63)
 };
-static_assert(sizeof(Smem<16>) <= 160 * 1024, "LDS budget");
+static_assert(sizeof(Smem) <= 160 * 1024, "LDS budget");
 
 // acc[ot] += W[ot tile] . b over k-steps u = 0..7 in order (the resident kernel's per-accumulator
 // sequence: common.hpp gemm); fragments (u, ot) stream PF deep, ot inner
@@ -99,18 +106,10 @@ __device__ unsigned long long* agn_e32_stamps;
   } while (0)
 #endif
 
-// s_setprio takes an immediate
-AGN_DEV void set_prio(int p) {
-  if (p == 1) __builtin_amdgcn_s_setprio(1);
-  else if (p == 2) __builtin_amdgcn_s_setprio(2);
-  else if (p == 3) __builtin_amdgcn_s_setprio(3);
-}
-
-template <int NW, int PRIO>
+template <bool SAVE>
 __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_args a) {
   constexpr int NTHR = 64 * NW;
-  constexpr bool KEEP_E = NW <= 12;  // the residual: kept operand, or re-read in the epilogue
-  __shared__ Smem<NW> sm;
+  __shared__ Smem sm;
   {
     const uint4* const* wp = reinterpret_cast<const uint4* const*>(a.wpk);
     for (int i = threadIdx.x; i < 4 * LAYER; i += NTHR) sm.w[i] = wp[i / LAYER][i % LAYER];
@@ -122,11 +121,6 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
   __syncthreads();
   const int lane0 = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // waves w, w + 4, w + 8 (, w + 12) share a SIMD (dispatched to the 4 SIMDs in turn): PRIO 1 ranks
-  // them by that order, PRIO 2 the reverse, so the three chains drift apart instead of running
-  // their MFMA and VALU phases in step (MI355X_MICROARCH.md, two waves per SIMD, items 4 and 9)
-  if constexpr (PRIO == 1) set_prio(w >> 2);
-  if constexpr (PRIO == 2) set_prio(NW / 4 - 1 - (w >> 2));
   const int ntiles = (a.rows + 31) / 32;
   const Walk walk(ntiles, w, NW);
   int* wids = sm.ids[w];
@@ -166,6 +160,10 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
         rd[i] = *reinterpret_cast<const uint4*>(pd + 16 * i);
       }
       b.load_w(E + (size_t)rr * H, h);
+      // all 24 row loads in flight before the first use: without this fence the scheduler of the
+      // SAVE instantiation (a1 / statistics stores, 152 registers) issued the P_d rows two at a time
+      // behind vmcnt(0) waits (1.01 -> 1.46 ms per C3 launch)
+      __builtin_amdgcn_sched_barrier(0);
       xs.set_w(rs);
       xd.set_w(rd);
       bf16x8 f0, f1;
@@ -181,14 +179,24 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       }
     }
     E32_STAMP(1);
-    BOp<bf16, NR> e0;
-    if constexpr (KEEP_E) e0 = b;
+    const BOp<bf16, NR> e0 = b;  // the residual operand
     gemm4(acc, b, sm.w, lane);
     E32_STAMP(2);
 #pragma unroll
     for (int l = 1; l < 4; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
+      if constexpr (SAVE && AGN_E32_A1 == 0) {
+        if (l == 1) b.store_tiled(reinterpret_cast<bf16*>(a.act[0]), row, h, valid);  // a1 (AGN_TILED)
+      }
+      if constexpr (SAVE && AGN_E32_A1 == 2) {  // (A/B: non-temporal stores)
+        if (l == 1 && valid) {
+          u32x4* base = reinterpret_cast<u32x4*>(a.act[0]);
+#pragma unroll
+          for (int i = 0; i < NR / 8; ++i)
+            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, b.u[i]), base + tiled_unit<bf16, NR>(row, i, h));
+        }
+      }
 #pragma unroll
       for (int q = 0; q < 4 * NT; ++q) {  // acc = bias of Linear l (mlp.hip acc_bias_lds)
         const f32x4 x = *reinterpret_cast<const f32x4*>(&sm.pv[l - 1][8 * q + 4 * h]);
@@ -196,6 +204,9 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
         for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
       }
       gemm4(acc, b, sm.w + l * LAYER, lane);
+      if constexpr (SAVE && AGN_E32_A1 == 1) {  // (A/B: a1 stored behind the Lin1 MFMAs)
+        if (l == 1) b.store_tiled(reinterpret_cast<bf16*>(a.act[0]), row, h, valid);
+      }
       E32_STAMP(2 + l);
     }
     cbarrier();
@@ -210,8 +221,10 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
     for (int i = 0; i < (AGN_E32_DIAG == 1 ? 2 : NR); i += 2) q = ln_sq_acc2(q, acc[i / 16][i % 16], acc[(i + 1) / 16][(i + 1) % 16], mean);
     q = sum32(q);
     const float rstd = 1.0f / sqrtf(q / (float)H + 1e-5f);
+    if constexpr (SAVE) {
+      if (h == 0 && valid) *reinterpret_cast<f32x2*>(a.stats + 2 * (size_t)row) = f32x2{mean, rstd};
+    }
     E32_STAMP(6);
-    const bf16* rp = E + (size_t)rr * H;
     bf16* op = reinterpret_cast<bf16*>(a.out) + (size_t)row * H;
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
@@ -232,8 +245,7 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
         }
       }
       float r[8];
-      if constexpr (KEEP_E) e0.get8(r, i);
-      else load8_w(r, rp, i, h);
+      e0.get8(r, i);
 #pragma unroll
       for (int e = 0; e < (AGN_E32_DIAG == 2 ? 0 : 8); e += 2) {  // round(LN) + residual, rounded again at the store
         const uint32_t p = pack2(v[e], v[e + 1]);
@@ -270,38 +282,6 @@ bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 
-namespace agn {
-// agn_set_option(AGN_OPT_EDGE_FWD32_WAVES / _PRIO) (mlp.hip)
-int edge32_fwd_set_option(int key, int value) {
-  if (key == AGN_OPT_EDGE_FWD32_WAVES) {
-    const int old = g_nw;
-    if (value != 12 && value != 16) return AGN_E_ARG;
-    g_nw = value;
-    return old;
-  }
-  if (key == AGN_OPT_EDGE_FWD32_PRIO) {
-    const int old = g_prio;
-    if (value < 0 || value > 2) return AGN_E_ARG;
-    g_prio = value;
-    return old;
-  }
-  return AGN_E_ARG;
-}
-}  // namespace agn
-
-namespace {
-template <int NW, int PRIO>
-void launch(const agn_edge_fwd_args* a, void* stream) {
-  hipLaunchKernelGGL((edge32_fwd_kernel<NW, PRIO>), dim3(a->nblk), dim3(64 * NW), 0, (hipStream_t)stream, *a);
-}
-template <int NW>
-void launch_p(const agn_edge_fwd_args* a, void* stream) {
-  if (g_prio == 1) launch<NW, 1>(a, stream);
-  else if (g_prio == 2) launch<NW, 2>(a, stream);
-  else launch<NW, 0>(a, stream);
-}
-}  // namespace
-
 extern "C" {
 
 #ifdef AGN_E32_STAMPS
@@ -313,7 +293,7 @@ int agn_debug_e32_stamps(void* p) {
 int agn_edge_fwd32_blocks(int rows) {
   const int cus = cu_count();
   const int tiles = (rows + 31) / 32;
-  const int need = (tiles + g_nw - 1) / g_nw;
+  const int need = (tiles + NW - 1) / NW;
   if (need >= cus) return cus;
   const int n = (need + 7) / 8 * 8;
   return n < 8 ? 8 : n;
@@ -323,12 +303,15 @@ int agn_edge_forward32(const agn_edge_fwd_args* a, void* stream) {
   if (!a || a->rows < 0 || a->nblk < 1) return AGN_E_ARG;
   if (a->rows == 0) return 0;
   if (!a->e || !a->proj || !a->src || !a->dst || !a->out || !a->ln_g || !a->ln_b) return AGN_E_ARG;
-  if (a->act[0] || a->act[1] || a->act[2] || a->hpre || a->stats) return AGN_E_ARG;  // no saves
+  if (a->act[1] || a->act[2] || a->hpre) return AGN_E_ARG;  // a1 and the statistics are the only saves
+  const bool save = a->act[0] != nullptr;
+  if (save != (a->stats != nullptr) || (save && (!al16(a->act[0]) || (reinterpret_cast<uintptr_t>(a->stats) & 7))))
+    return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l] || !al16(a->wpk[l])) return AGN_E_ARG;
   if (!al16(a->e) || !al16(a->proj) || !al16(a->out)) return AGN_E_ARG;
-  if (g_nw == 16) launch_p<16>(a, stream);
-  else launch_p<12>(a, stream);
+  if (save) hipLaunchKernelGGL(edge32_fwd_kernel<true>, dim3(a->nblk), dim3(64 * NW), 0, (hipStream_t)stream, *a);
+  else hipLaunchKernelGGL(edge32_fwd_kernel<false>, dim3(a->nblk), dim3(64 * NW), 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

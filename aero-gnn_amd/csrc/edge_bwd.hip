@@ -43,7 +43,19 @@ constexpr int NR = 64;                 // acc registers per row half
 constexpr int CW = 4;                  // chain waves
 constexpr int NWAVE = 8;               // chain + dW waves
 constexpr int NTHR = 64 * NWAVE;
-constexpr int NSLOT = 3;
+#ifndef AGN_EB_RELOAD_LATE
+#define AGN_EB_RELOAD_LATE 0  // (A/B) the g / g2 re-reads for de issued after the L1 hand-off instead of before it
+#endif
+#ifndef AGN_EB_WE_LDS
+#define AGN_EB_WE_LDS 0  // (A/B) W_e's image in LDS (the round-5 layout, 3 ring slots) instead of L2 fragments
+#endif
+#ifndef AGN_EB_G0_EARLY
+#define AGN_EB_G0_EARLY 0  // (A/B) G0 stored before de's W_e GEMM (round 5 order) instead of after it
+#endif
+#ifndef AGN_EB_NSLOT
+#define AGN_EB_NSLOT (AGN_EB_WE_LDS ? 3 : 7)
+#endif
+constexpr int NSLOT = AGN_EB_NSLOT;    // ring slots (8 KB each; a tile's hand-off pair takes two)
 #ifndef AGN_EB_GROUP
 #define AGN_EB_GROUP 2  // chain waves per hand-off group (item order, chain_wave)
 #endif
@@ -51,10 +63,13 @@ constexpr int GROUP = AGN_EB_GROUP;
 constexpr int IMG_B = H * H * 2;       // one 128 x 128 bf16 image (32 KB)
 constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
 constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
-constexpr int OFF_RING = 4 * IMG_B;
+// LDS images of Lin1..Lin3 at (l - 1) * IMG_B; W_e is read from L2 (packed fragments, 32 KB shared by
+// every CU): its 32 KB of LDS went to the ring, 3 -> 7 slots (round 6)
+constexpr int IMG1 = AGN_EB_WE_LDS ? 1 : 0;  // image index of Lin1 (W_e at 0 when it is in LDS)
+constexpr int OFF_RING = (3 + IMG1) * IMG_B;
 constexpr int OFF_PV = OFF_RING + NSLOT * SLOT_B;  // fp32 [4][H]: b1, b2, b3, LN gamma
-constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[4], consumed[4]
-constexpr int OFF_LNP = OFF_FLAG + 32;             // fp32 [CW][2][H]: LayerNorm partials per chain wave
+constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[NSLOT], consumed[NSLOT]
+constexpr int OFF_LNP = OFF_FLAG + 8 * ((2 * NSLOT + 7) / 8) * 4;  // fp32 [CW][2][H]: LayerNorm partials per chain wave
 constexpr int OFF_IDS = OFF_LNP + CW * 2 * H * 4;   // int [CW][64]: next tile's src (lanes 0-31) / dst
 constexpr int LDS_B = OFF_IDS + CW * 64 * 4;
 static_assert(LDS_B <= 160 * 1024, "LDS budget");
@@ -135,6 +150,40 @@ AGN_DEV void gemm_cols(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const char* im
   }
 }
 
+// gemm_rows and gemm_cols with the A fragments from global memory (L2): W_e's packed operands,
+// forward (agn_pack trans = 0) and transposed (trans = 1), unit ((ot * 8) + u) * 64 + lane. These are
+// the values the LDS image reads give (the image is built from the trans = 0 operand; the transposed
+// reads reproduce the trans = 1 operand, see gemm_cols), in the same MFMA order: bitwise the same sums.
+// Fragments stream PFG deep (L2 latency under the MFMAs).
+constexpr int PFG = 8;
+AGN_DEV void gemm_rows_g(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const uint4* w, int lane) {
+  uint4 f[PFG];
+#pragma unroll
+  for (int i = 0; i < PFG; ++i) f[i] = w[((i & 3) * 8 + (i >> 2)) * 64 + lane];
+#pragma unroll
+  for (int idx = 0; idx < 8 * NT; ++idx) {
+    const uint4 cur = f[idx % PFG];
+    const int nx = idx + PFG;
+    if (nx < 8 * NT) f[idx % PFG] = w[((nx & 3) * 8 + (nx >> 2)) * 64 + lane];
+    b.mfma(acc[idx & 3], cur, idx >> 2);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+AGN_DEV void gemm_cols_g(f32x16 (&acc)[NT], const BOp<bf16, NR>& b, const uint4* wt, int lane) {
+  uint4 f[PFG];
+#pragma unroll
+  for (int i = 0; i < PFG; ++i) f[i] = wt[((i & 3) * 8 + (i >> 2)) * 64 + lane];
+#pragma unroll
+  for (int idx = 0; idx < 8 * NT; ++idx) {
+    const bf16x8 cur = __builtin_bit_cast(bf16x8, f[idx % PFG]);
+    const int nx = idx + PFG;
+    if (nx < 8 * NT) f[idx % PFG] = wt[((nx & 3) * 8 + (nx >> 2)) * 64 + lane];
+    if (idx < NT) acc[idx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cur, b.u[0], f32x16{}, 0, 0, 0);
+    else mfma(acc[idx & 3], cur, b.u[idx >> 2]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // acc = bias (fp32 [H] in LDS), acc layout
 AGN_DEV void acc_bias(f32x16 (&acc)[NT], const float* pv, int h) {
 #pragma unroll
@@ -208,7 +257,7 @@ AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<b
   return;  // diagnostic build only: the chain alone (no hand-offs; dW / db are not computed)
 #endif
   int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
-  int* consumed = filled + 4;
+  int* consumed = filled + NSLOT;
   const int k0 = n0 % NSLOT, j0 = n0 / NSLOT;
   const int k1 = (n0 + 1) % NSLOT, j1 = (n0 + 1) / NSLOT;
 #ifdef AGN_EB_STAMPS
@@ -284,6 +333,13 @@ AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const B
 #define EB_IST(pi) nullptr
 #endif
 
+// SAVED: the tile starts from the forward's a1 (AGN_TILED) and LayerNorm statistics
+// (agn_edge_forward32's training saves) instead of recomputing h0 from e, P_s[src], P_d[dst] and
+// W_e; every value downstream is bitwise the same. SCR: a2 and a3 of the recompute go to the wave's
+// 16-KB slice of a.scratch (L2-resident: the same addresses are rewritten every tile) and are read
+// back for their hand-offs, instead of being recomputed from a1 a second time (64 MFMAs plus their
+// bias / ReLU work per tile).
+template <bool SAVED, bool SCR>
 AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0) {
 #ifdef AGN_EB_STAMPS
   unsigned long long* stp = nullptr;
@@ -307,9 +363,12 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   auto tile_id = [&](int rd) {
     const int row = (rd * CW + cw) * 32 + (lane0 & 31);
     const int rr = row < a.rows ? row : a.rows - 1;
-    const int32_t* p = lane0 < 32 ? srcp : dstp;
+    const int32_t* p = (lane0 < 32 && !SAVED) ? srcp : dstp;  // (SAVED reads no src)
     return p[rr];
   };
+  // this wave's scratch slice: a2 at +0, a3 at +8 KB, unit i of lane l at 16 (64 i + l) (1 KB per
+  // wave instruction)
+  uint4* const scr = SCR ? reinterpret_cast<uint4*>(a.scratch) + (size_t)(blockIdx.x * CW + cw) * 1024 : nullptr;
   if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
 
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
@@ -332,11 +391,20 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
-    const int sid = ids[c], did = ids[32 + c];
+    const int sid = SAVED ? 0 : ids[c], did = ids[32 + c];
     const bool more = rd + rw.step < rw.end;
     const int nid = tile_id(more ? rd + rw.step : rd);  // stored to the slot before the tile's stores
     // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
     // forward recompute
+    // SAVED: a1 and the statistics first (the recompute starts on a1)
+    BOp<bf16, NR> a1;  // the only activation kept in registers from the forward pass
+    f32x2 st{0.f, 0.f};
+    if constexpr (SAVED) {
+      const uint4* ap = reinterpret_cast<const uint4*>(a.a1);
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) a1.u[i] = __builtin_bit_cast(bf16x8, ap[tiled_unit<bf16, NR>(rr, i, h)]);
+      st = *reinterpret_cast<const f32x2*>(a.stats + 2 * (size_t)rr);
+    }
     uint4 graw[NR / 8], g2raw[NR / 8];
     {
       const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H;
@@ -353,49 +421,66 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     }
     // ---- forward recompute (mlp_fwd_res_kernel's operations, in its order)
     f32x16 acc[NT];
-    BOp<bf16, NR> a1;  // the only activation kept from the forward pass
-    {
-      {  // acc = P_s[src] + P_d[dst] on the matrix cores (the forward kernel's exact add)
-        BOp<bf16, NR> xs, xd;
-        xs.load_w(P + (size_t)sid * (2 * H), h);
-        xd.load_w(P + (size_t)did * (2 * H) + H, h);
-        bf16x8 f0, f1;
-        ident_frags(f0, f1, fresh_lane(lane));
-        acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+    if constexpr (!SAVED) {
+      {
+        {  // acc = P_s[src] + P_d[dst] on the matrix cores (the forward kernel's exact add)
+          BOp<bf16, NR> xs, xd;
+          xs.load_w(P + (size_t)sid * (2 * H), h);
+          xd.load_w(P + (size_t)did * (2 * H) + H, h);
+          bf16x8 f0, f1;
+          ident_frags(f0, f1, fresh_lane(lane));
+          acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+        }
+        BOp<bf16, NR> eop;
+        eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
+        EB_STAMP(1);
+        if (AGN_EB_WE_LDS) gemm_rows(acc, eop, lds, fresh_lane(lane));
+        else gemm_rows_g(acc, eop, reinterpret_cast<const uint4*>(a.wpk[0]), fresh_lane(lane));
       }
-      BOp<bf16, NR> eop;
-      eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
+      cbarrier();
+      a1.template set_relu<NT>(acc);
+    } else {
       EB_STAMP(1);
-      gemm_rows(acc, eop, lds + 0 * IMG_B, fresh_lane(lane));
     }
-    cbarrier();
-    a1.template set_relu<NT>(acc);
     pin(a1);
     sched_fence();
     acc_bias(acc, pv + 0 * H, h);
-    gemm_rows(acc, a1, lds + 1 * IMG_B, fresh_lane(lane));
+    gemm_rows(acc, a1, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
     cbarrier();
-    {  // a2 is not kept (recomputed from a1 in step 2: 32 MFMAs instead of 32 live registers)
+    {  // a2 is not kept (recomputed from a1 in step 2, or parked in the scratch)
       BOp<bf16, NR> a2;
       a2.template set_relu<NT>(acc);
       pin(a2);
+      if constexpr (SCR) {
+        const int l = fresh_lane(lane);
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) scr[64 * i + l] = __builtin_bit_cast(uint4, a2.u[i]);
+      }
       sched_fence();
       acc_bias(acc, pv + 1 * H, h);
-      gemm_rows(acc, a2, lds + 2 * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a2, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
     }
     cbarrier();
-    {  // a3 is not kept either (recomputed in step 3)
+    {  // a3 is not kept either (recomputed in step 3, or parked in the scratch)
       BOp<bf16, NR> a3;
       a3.template set_relu<NT>(acc);
       pin(a3);
+      if constexpr (SCR) {
+        const int l = fresh_lane(lane);
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) scr[512 + 64 * i + l] = __builtin_bit_cast(uint4, a3.u[i]);
+      }
       sched_fence();
       acc_bias(acc, pv + 2 * H, h);
-      gemm_rows(acc, a3, lds + 3 * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a3, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
     }
     EB_STAMP(2);
     // LayerNorm statistics (mlp_fwd_res_kernel's epilogue)
     float mean, rstd;
-    {
+    if constexpr (SAVED) {
+      mean = st[0];
+      rstd = st[1];
+    } else {
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < NR; ++i) s += acc[i / 16][i % 16];
@@ -435,6 +520,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     }
     // ---- LayerNorm backward (mlp_bwd_res_kernel, its expressions; partials in 16-register
     // chunks: the butterfly's XOR order 16, 8, 4, 2, 1 gives each feature the same sums)
+    BOp<bf16, NR> a3s;  // SCR: a3 read back
     {
       const float* gmv = pv + 3 * H;
       // this wave's LayerNorm parameter partials: lane c adds sum g * xhat (c < 16) or sum g
@@ -480,6 +566,11 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       c2 = sum32(c2);
       c1 /= (float)H;
       c2 /= (float)H;
+      if constexpr (SCR) {  // a3 back from the scratch, under the second pass
+        const int l = fresh_lane(lane);
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) a3s.u[i] = __builtin_bit_cast(bf16x8, scr[512 + 64 * i + l]);
+      }
       // pass 2 unpacks h3 and recomputes xhat again: opaque copies keep the compiler from holding
       // pass 1's 64 unpacked / normalised values live in between
       opaque(mean);
@@ -515,18 +606,32 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     op.set(A);  // G3
     pin(op);
     BOp<bf16, NR> a2;
-    {
+    if constexpr (SCR) {
+      pin(a3s);
+      EB_STAMP(4);
+      produce_pair(lds, nbase + 0 * gsz, op, a3s, fresh_lane(lane), EB_IST(0));
+      {  // a2 back from the scratch, under the chain step
+        const int l = fresh_lane(lane);
+#pragma unroll
+        for (int i = 0; i < NR / 8; ++i) a2.u[i] = __builtin_bit_cast(bf16x8, scr[64 * i + l]);
+      }
+      EB_STAMP(5);
+      gemm_cols(acc, op, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
+      cbarrier();
+      relu_select_pk(op, acc, a3s);  // G2
+      EB_STAMP(6);
+    } else {
       // a2 = relu(a1 W1^T + b1), a3 = relu(a2 W2^T + b2) again (the forward's operations)
       BOp<bf16, NR> a3;
       sched_fence();
       acc_bias(acc, pv + 0 * H, h);
-      gemm_rows(acc, a1, lds + 1 * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a1, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
       cbarrier();
       a2.template set_relu<NT>(acc);
       pin(a2);
       sched_fence();
       acc_bias(acc, pv + 1 * H, h);
-      gemm_rows(acc, a2, lds + 2 * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a2, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
       cbarrier();
       a3.template set_relu<NT>(acc);
       pin(a3);
@@ -534,7 +639,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       EB_STAMP(4);
       produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
       EB_STAMP(5);
-      gemm_cols(acc, op, lds + 3 * IMG_B, fresh_lane(lane));
+      gemm_cols(acc, op, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
       cbarrier();
       relu_select_pk(op, acc, a3);  // G2
       EB_STAMP(6);
@@ -542,7 +647,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
-    gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
+    gemm_cols(acc, op, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a2);  // G1
     EB_STAMP(8);
@@ -550,7 +655,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     // de = G0 W_e + (g + g2) (mlp_bwd_res_kernel's add_grad_w order) needs the incoming rows
     // again: re-read now (L2) so the loads complete under the L1 hand-off and chain step.
     // Opaque indices keep the compiler from holding the first reads' values live since the LN.
-    {
+    auto reload_g = [&]() {
       int did2 = did, rr2 = rr;
       opaque(did2);
       opaque(rr2);
@@ -562,17 +667,24 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
 #pragma unroll
         for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
       }
-    }
+    };
+    if (!AGN_EB_RELOAD_LATE) reload_g();
     produce_pair(lds, nbase + 4 * gsz, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
-    gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
+    if (AGN_EB_RELOAD_LATE) reload_g();
+    gemm_cols(acc, op, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a1);  // G0
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
-    op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
-    gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
+    // de = G0 W_e first, G0's stores after it: vmcnt retires loads and stores in issue order, so W_e's
+    // fragment loads issued behind the G0 stores would each wait for those stores too
+    if (AGN_EB_G0_EARLY) op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
+    if (AGN_EB_WE_LDS) gemm_cols(acc, op, lds, fresh_lane(lane));
+    else gemm_cols_g(acc, op, reinterpret_cast<const uint4*>(a.wtpk0), fresh_lane(lane));
+    sched_fence();
+    if (!AGN_EB_G0_EARLY) op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     {
       float v[NR];
 #pragma unroll
@@ -597,265 +709,13 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   }
 }
 
-// ------------------------------------------------------------------------------ dP_d
-// P_d = x W_d^T + b enters h0 of every edge of its receiver (mgnLayer.py:72-105), so dP_d[n] is
-// the sum of G0 over n's edges: agn_segment_sum's fp32 sum in edge order from zero, rounded once.
-// The dW waves form it on chip: dW wave d recomputes features 32d..32d+31 of G0 for each tile
-// from the tile's L1 hand-off (G1, a1) and walks the tile's 32 rows in order, carrying the open
-// receiver's sum from tile to tile of a round (the L1 pairs arrive in tile order) and restarting
-// it at every change of receiver. The walk stores the running sum of EVERY row to dP_d[dst[row]]:
-// one wave's stores to one address land in program order, so a receiver's last store is its
-// whole sum, and the walk needs no branch per row. Receivers whose edges span a 128-row round
-// boundary get partial sums from two rounds; dpd_cross_kernel, launched after the fused kernel,
-// overwrites them (and writes the empty receivers' zeros).
-constexpr int ROUND_ROWS = CW * 32;
-
-struct DpdWalk {
-  int cur;    // receiver of the open run (-1 at a round's start: the round's first row opens one)
-  float sum;  // its fp32 sum (lanes 0-31: feature 32d + lane)
-#ifdef AGN_EB_STAMPS
-  unsigned long long t_mm = 0, t_walk = 0;  // cycles in the G0 recompute (to the release) / the walk
-#endif
-};
-
-// The receiver ids are read with scalar loads (constant address space: s_load, counted by lgkmcnt).
-// A vector load would be waited for with vmcnt, which also counts the walk's own dP_d stores: every
-// walk would then wait for the previous walk's 32 stores to be acknowledged.
-typedef __attribute__((address_space(4))) const int32_t cint32;
-
-// one row of the sequential walk (the last, partial tile of an edge list): restart the sum at a new
-// receiver, add the row, store the running sum (lanes 0-31: a uniform row base, 32-bit lane offset)
-AGN_DEV void dpd_row(const agn_edge_bwd_args& a, DpdWalk& st, int n, float v, int d, int lane) {
-  st.sum = (n != st.cur ? 0.f : st.sum) + v;
-  st.cur = n;
-  bf16* rowp = reinterpret_cast<bf16*>(a.dpd) + ((size_t)n * H + 32 * d);
-  if (lane < 32) rowp[lane] = (bf16)st.sum;
-}
-
-// dP_d of a tile's L1 pair (ring slots k0, k1), then release() the slots. The ring reads stream
-// under the MFMAs (one fragment in flight: the dW wave's 192 accumulators leave no room to hold
-// the pair's 40 registers of G1 / a1 across a release) and the slots are released after the
-// last MFMA, before the row walk.
-template <typename Release>
-AGN_DEV void dpd_pair(const agn_edge_bwd_args& a, const char* lds, int k0, int k1, int tile, int d, int lane,
-                      DpdWalk& st, Release release) {
-#ifdef AGN_EB_STAMPS
-  const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-#endif
-  lane = fresh_lane(lane);  // lane-derived offsets are formed here, not hoisted out of the dW loop
-  const int c = lane & 31, hh = lane >> 5;
-  // the tile's 32 receivers: contiguous scalar loads (two s_load_dwordx16), their latency under the
-  // MFMAs below. The last tile of the edge list, if partial, reads them with a vector load (clamped
-  // rows) and pays its wait once.
-  const int row0 = tile * 32;
-  const int nval = min(32, a.rows - row0);
-  const bool full = nval == 32;
-  int ids[32];
-  int dvec = 0;
-  if (full) {
-    cint32* dsc = (cint32*)(a.dst) + row0;  // (a C-style cast: the address-space conversion)
-#pragma unroll
-    for (int r = 0; r < 32; ++r) ids[r] = dsc[r];
-  } else {
-    dvec = a.dst[min(row0 + c, a.rows - 1)];
-  }
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  // [a1 > 0] at D's places, as 16 bits: transposed reads of the items' a1 images. Register 4m + j
-  // of lane (c, hh) is row 8m + 4hh + j, feature 32d + c; lane 4j + p of each 16-lane group
-  // supplies row 8m + 4hh + j at image positions 32d + 16(g&1) + 4 sw(p) (sw swaps p's bits: phi),
-  // so lane t of the group receives feature 32d + 16(g&1) + t. Relu outputs are +0 or positive
-  // int16 patterns (relu_select_pk's mask rule).
-  int keep = 0;
-  {
-    const int xm = 2 * (g & 1) + (p & 1);
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const char* sa = lds + OFF_RING + ((m >> 1) ? k1 : k0) * SLOT_B + HALF_B;
-      const int off = 2048 * (m & 1) + 512 * d + 64 * (4 * hh + q) + 16 * (xm ^ (2 * (m & 1) + hh)) + 8 * (p >> 1);
-      const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(sa + off));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) keep |= (v[j] > 0 ? 1 : 0) << (4 * m + j);
-    }
-  }
-  // D[row c'][f] = sum_k G1[c'][k] W1[k][32d + f]: the chain's last gemm_cols step (ot = d) with the
-  // operands swapped: A = the chain's own G1 operand read back from the ring (lane (c, hh) of k-step
-  // u: chunk 2u + hh of row c), B = gemm_cols' W1^T fragment. Same products, same k order, so D is
-  // the transpose of the chain's accumulator, bitwise.
-  f32x16 D;
-  {
-    const char* sg = lds + OFF_RING + ((c >> 4) ? k1 : k0) * SLOT_B;
-    const int r = c & 15, x = (r >> 2) & 3;
-    const int base = 2048 * (r >> 3) + 64 * (r & 7);
-    const int oe = base + 16 * (hh ^ x), oo = base + 16 * ((2 + hh) ^ x);
-    const int xx = 2 * (g & 1) + (p & 1);
-    const char* img = lds + 1 * IMG_B + 512 * d;
-    const char* r1 = img + 64 * (4 * hh + q) + 16 * (xx ^ hh) + 8 * (p >> 1);
-    const char* r2 = img + 2048 + 64 * (4 * hh + q) + 16 * (xx ^ (hh + 2)) + 8 * (p >> 1);
-    auto ga = [&](int u) { return *reinterpret_cast<const uint4*>(sg + (u & 1 ? oo : oe) + 512 * (u >> 1)); };
-    auto wb = [&](int u) { return tr_pair(r1 + 4096 * u, r2 + 4096 * u); };
-    uint4 a0 = ga(0);
-    bf16x8 b0 = wb(0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint4 ca = a0;
-      const bf16x8 cb = b0;
-      if (u + 1 < 8) {
-        a0 = ga(u + 1);
-        b0 = wb(u + 1);
-      }
-      D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, ca), cb, u == 0 ? f32x16{} : D, 0, 0, 0);
-      sched_fence();
-    }
-  }
-  lgkm_drain();
-  release();
-#ifdef AGN_EB_STAMPS
-  const unsigned long long c1 = __builtin_amdgcn_s_memtime();
-  st.t_mm += c1 - c0;
-#endif
-  // The walk below is VALU work that holds up nothing: it runs at the chain wave's priority, so it
-  // takes the SIMD's issue cycles the (issue-bound) chain wave leaves idle instead of preempting it
-  __builtin_amdgcn_s_setprio(0);
-  // G0 = round(D) where a1 > 0
-  float gv[16];
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const uint32_t pk = pack2(D[k], D[k + 1]);
-    gv[k] = (keep >> k) & 1 ? lo_bf16(pk) : 0.f;
-    gv[k + 1] = (keep >> (k + 1)) & 1 ? hi_bf16(pk) : 0.f;
-  }
-  if (full) {
-    // Two halves in lockstep. swap(a, b) = (a.lo | b.lo, a.hi | b.hi) of v_permlane32_swap puts
-    // rows 0-15 in lanes 0-31 and rows 16-31 in lanes 32-63, same features: local row r = 8m + j
-    // of either half is A[4m + j] (j < 4) or B[4m + j - 4] (j >= 4).
-    float A[8], B[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[k]), __float_as_uint(gv[k + 8]), false, false);
-      A[k] = __uint_as_float(sw[0]);
-      B[k] = __uint_as_float(sw[1]);
-    }
-    auto row_v = [&](int r) { return (r & 7) < 4 ? A[4 * (r >> 3) + (r & 7)] : B[4 * (r >> 3) + (r & 7) - 4]; };
-    // byte offset of (receiver n, this lane's feature) in dP_d: 32-bit (nodes < 2^24), so the store
-    // takes the scalar base + vector offset form
-    const uint32_t voff = 64 * d + 2 * c;
-    char* const dpb = reinterpret_cast<char*>(a.dpd);
-    auto put = [&](int n, float v) { *reinterpret_cast<bf16*>(dpb + ((uint32_t)n * (H * 2) + voff)) = (bf16)v; };
-    // the open run per lane: lanes 0-31 carry it from the previous tile, lanes 32-63 open one at row 16
-    int cur = hh ? -1 : st.cur;
-    float sum = st.sum;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = hh ? ids[16 + r] : ids[r];
-      sum = (n != cur ? 0.f : sum) + row_v(r);
-      cur = n;
-      put(n, sum);
-    }
-    // Rows 15 and 16 of one receiver: the upper half summed that run from zero above. Redo it from
-    // the lower half's sum, in row order (these stores land after the walk's, so they stand).
-    if (ids[16] == ids[15]) {
-      float s2 = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false)[0]);
-      bool through = true;  // the run covers rows 16-31: it is the tile's open run
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (ids[16 + r] != ids[15]) {
-          through = false;
-          break;
-        }
-        s2 += row_v(r);
-        if (hh) put(ids[15], s2);
-      }
-      if (through) sum = s2;
-    }
-    // the tile's open run (row 31's receiver) goes to the next tile in lanes 0-31
-    st.sum = __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false)[1]);
-    st.cur = ids[31];
-  } else {
-    // rows in order: 8m + j is register 4m + j of lanes 0-31, 8m + 4 + j that of lanes 32-63, which
-    // lanes 0-31 take over by v_permlane32_swap, four registers at a time
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = gv[4 * m + j];
-        v[4 + j] = __uint_as_float(
-            __builtin_amdgcn_permlane32_swap(__float_as_uint(gv[4 * m + j]), __float_as_uint(gv[4 * m + j]), false, false)[1]);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (8 * m + j < nval) dpd_row(a, st, __builtin_amdgcn_readlane(dvec, 8 * m + j), v[j], d, lane);
-      sched_fence();
-    }
-  }
-  __builtin_amdgcn_s_setprio(2);
-#ifdef AGN_EB_STAMPS
-  st.t_walk += __builtin_amdgcn_s_memtime() - c1;
-#endif
-}
-
-// receivers the in-kernel walk does not finish (edges spanning a round boundary: the walk left
-// partial sums there) and empty ones, after the fused kernel: segment_sum_kernel's summation
-// order (16 threads per receiver, 8 features each). A block checks 256 receivers (one per thread),
-// lists the few that need it (about one in twenty at C3's level 0) and sums those 16 at a time:
-// the check alone used to take 16 threads per receiver (62 us per C3 launch)
-__global__ __launch_bounds__(256) void dpd_cross_kernel(int nodes, const int32_t* __restrict__ ptr,
-                                                        const bf16* __restrict__ g0, bf16* __restrict__ dpd) {
-  __shared__ int list[256];
-  __shared__ int cnt;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  {
-    const int n = blockIdx.x * 256 + threadIdx.x;
-    if (n < nodes) {
-      const int beg = ptr[n], end = ptr[n + 1];
-      if (!(end > beg && beg / ROUND_ROWS == (end - 1) / ROUND_ROWS)) list[atomicAdd(&cnt, 1)] = n;
-    }
-  }
-  __syncthreads();
-  const int total = cnt;
-  const int sub = threadIdx.x & 15;
-  const int f0 = 8 * sub;
-  auto ld8 = [&](float (&o)[8], int row) {
-    const u32x4 x = *reinterpret_cast<const u32x4*>(g0 + (size_t)row * H + f0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      o[2 * i] = lo_bf16(x[i]);
-      o[2 * i + 1] = hi_bf16(x[i]);
-    }
-  };
-  for (int li = threadIdx.x >> 4; li < total; li += 16) {
-    const int n = list[li];
-    const int beg = ptr[n], end = ptr[n + 1];
-    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int j = beg;
-    for (; j + 1 < end; j += 2) {
-      float x[8], y[8];
-      ld8(x, j);
-      ld8(y, j + 1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] = (s[i] + x[i]) + y[i];
-    }
-    if (j < end) {
-      float x[8];
-      ld8(x, j);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s[i] += x[i];
-    }
-    u32x4 w;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = pack2(s[2 * i], s[2 * i + 1]);
-    *reinterpret_cast<u32x4*>(dpd + (size_t)n * H + f0) = w;
-  }
-}
-
 // ------------------------------------------------------------------------------ dW wave
 AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
 #ifdef AGN_EB_NORING
   return;  // diagnostic build only (see produce_pair)
 #endif
   int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
-  int* consumed = filled + 4;
+  int* consumed = filled + NSLOT;
   const int ntiles = (a.rows + 31) / 32;
   const int nrounds = (ntiles + CW - 1) / CW;
   const Rounds rw(nrounds);
@@ -884,10 +744,8 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   unsigned long long waited = 0;
   const unsigned long long tstart = __builtin_amdgcn_s_memtime();
 #endif
-  DpdWalk dw_run{-1, 0.f};
   for (int rd = rw.first; rd < rw.end; rd += rw.step) {
     const int cmax = min(CW, ntiles - rd * CW);
-    dw_run.cur = -1;  // a round's first row opens a run (one that began earlier is dpd_cross_kernel's)
     for (int grp = 0; grp < CW / GROUP; ++grp) {  // the chain waves' item order (chain_wave): group, layer, wave
     const int gsz = GROUP == 2 ? (grp == 0 ? min(2, cmax) : max(0, cmax - 2)) : (grp < cmax ? 1 : 0);
 #pragma unroll
@@ -922,15 +780,10 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
           xf[q2][1] = tr_pair(sb + HALF_B + 512 * (ib + 1) + t1, sb + HALF_B + 512 * (ib + 1) + t2);
         }
         lgkm_drain();
-        auto release = [&]() {
-          if (lane == 0) {
-            __hip_atomic_fetch_add(&consumed[k0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(&consumed[k1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-        };
-        // an L1 pair with dP_d is released after its dP_d reads (dpd_pair)
-        const bool dp = li == 2 && a.dpd;
-        if (!dp) release();
+        if (lane == 0) {
+          __hip_atomic_fetch_add(&consumed[k0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_fetch_add(&consumed[k1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
 #ifdef AGN_EB_STAMPS
         if (ist && lane == 0) ist[2] = ist[5] = __builtin_amdgcn_s_memtime();
 #endif
@@ -951,10 +804,6 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
             }
           }
         }
-        if (dp) {
-          sched_fence();  // the dW MFMAs have taken gf / xf before these reads claim registers
-          dpd_pair(a, lds, k0, k1, rd * CW + grp * GROUP + cc, d, lane, dw_run, release);  // (L1 pairs: tile order)
-        }
       }
     }
     }
@@ -965,8 +814,6 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
     sp[0] = waited;
     sp[1] = __builtin_amdgcn_s_memtime() - tstart;
     sp[2] = (unsigned long long)n;
-    sp[3] = dw_run.t_mm;
-    sp[4] = dw_run.t_walk;
   }
 #endif
   // partial slabs (true feature order): dW_L of workgroup b at dw_partial[(L-1) nblk + b][o][i]
@@ -994,16 +841,17 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   }
 }
 
+template <bool SAVED, bool SCR>
 __global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_bwd_args a) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_B];
   // weight images from the packed forward operands: unit (ot, ku, lane) -> row 32ot + lane%32,
   // chunk 2ku + lane/32
-  for (int l = 0; l < 4; ++l) {
+  for (int l = 1 - IMG1; l < 4; ++l) {
     const uint4* src = reinterpret_cast<const uint4*>(a.wpk[l]);
     for (int u = threadIdx.x; u < 2048; u += NTHR) {
       const int ln = u & 63, unit = u >> 6;
       const int o = 32 * (unit >> 3) + (ln & 31), ch = 2 * (unit & 7) + (ln >> 5);
-      *reinterpret_cast<uint4*>(lds + l * IMG_B + aoff(o, ch)) = src[u];
+      *reinterpret_cast<uint4*>(lds + (l - 1 + IMG1) * IMG_B + aoff(o, ch)) = src[u];
     }
   }
   float* pv = reinterpret_cast<float*>(lds + OFF_PV);
@@ -1011,12 +859,12 @@ __global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_
     const int l = i / H, f = i - l * H;
     pv[i] = l < 3 ? (a.bias[l + 1] ? a.bias[l + 1][f] : 0.f) : a.ln_g[f];
   }
-  if (threadIdx.x < 8) reinterpret_cast<int*>(lds + OFF_FLAG)[threadIdx.x] = 0;
+  if (threadIdx.x < 2 * NSLOT) reinterpret_cast<int*>(lds + OFF_FLAG)[threadIdx.x] = 0;
   for (int i = threadIdx.x; i < CW * 2 * H; i += NTHR) reinterpret_cast<float*>(lds + OFF_LNP)[i] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave < CW) chain_wave(a, lds, wave, lane);
+  if (wave < CW) chain_wave<SAVED, SCR>(a, lds, wave, lane);
   else dw_wave(a, lds, wave - CW, lane);
   __syncthreads();
   // LayerNorm parameter partials of the four chain waves, summed in wave order
@@ -1053,14 +901,17 @@ int agn_edge_bwd_blocks(int rows) {
   return n < 8 ? 8 : n;
 }
 
-int agn_e16_fault_status(int* value, int reset);
-int agn_e16_fault_status_async(int* host_pinned, void* stream);
+size_t agn_edge_bwd_scratch_bytes(int nblk) { return nblk > 0 ? (size_t)nblk * CW * 2 * 32 * H * 2 : 0; }
+
 int agn_fault_status_async(int* host_pinned, void* stream) {
   if (!host_pinned) return AGN_E_ARG;
   const hipError_t e = hipMemcpyFromSymbolAsync(host_pinned, HIP_SYMBOL(g_agn_fault), sizeof(int), 0,
                                                 hipMemcpyDeviceToHost, (hipStream_t)stream);
-  if (e != hipSuccess) return (int)e;
-  return agn_e16_fault_status_async(host_pinned + 1, stream);
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int agn_debug_set_fault(int value) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_agn_fault), &value, sizeof(int)) == hipSuccess ? 0 : AGN_E_ARG;
 }
 
 int agn_fault_status(int* value, int reset) {
@@ -1071,32 +922,28 @@ int agn_fault_status(int* value, int reset) {
     const int zero = 0;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_agn_fault), &zero, sizeof(int));
   }
-  int v16 = 0;
-  if (e == hipSuccess) {
-    const int r = agn_e16_fault_status(&v16, reset);
-    if (r != 0) return r;
-    *value |= v16;
-  }
   return e == hipSuccess ? 0 : (int)e;
 }
 
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
-  if (!a || a->rows < 1 || a->nblk < 1 || !a->e || !a->proj || !a->src || !a->dst || !a->g2 || !a->ln_g ||
-      !a->de || !a->g0 || !a->dw_partial || !a->db_partial || !a->ln_partial)
+  if (!a || a->rows < 1 || a->nblk < 1 || !a->dst || !a->g2 || !a->ln_g || !a->de || !a->g0 || !a->dw_partial ||
+      !a->db_partial || !a->ln_partial)
     return AGN_E_ARG;
+  // either the forward's saves (a1 AGN_TILED, 16-B aligned; stats 8-B aligned) or the recompute's inputs
+  if ((a->a1 != nullptr) != (a->stats != nullptr)) return AGN_E_ARG;
+  if (a->a1 ? ((reinterpret_cast<uintptr_t>(a->a1) & 15) || (reinterpret_cast<uintptr_t>(a->stats) & 7))
+            : (!a->e || !a->proj || !a->src))
+    return AGN_E_ARG;
+  if (a->scratch && (reinterpret_cast<uintptr_t>(a->scratch) & 15)) return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l]) return AGN_E_ARG;
-  // (the dP_d walk addresses rows with 32-bit byte offsets: nodes < 2^24)
-  if (a->dpd && (!a->rowptr || a->nodes < 1 || a->nodes >= (1 << 24) || (reinterpret_cast<uintptr_t>(a->dpd) & 15) ||
-                 (reinterpret_cast<uintptr_t>(a->g0) & 15)))
-    return AGN_E_ARG;
-  hipLaunchKernelGGL(edge_bwd_fused_kernel, dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
-  if (a->dpd) {
-    const int st = launch_status();
-    if (st) return st;
-    hipLaunchKernelGGL(dpd_cross_kernel, dim3((a->nodes + 255) / 256), dim3(256), 0, (hipStream_t)stream, a->nodes,
-                       a->rowptr, (const bf16*)a->g0, (bf16*)a->dpd);
-  }
+  if (!a->wtpk0) return AGN_E_ARG;
+  const bool saved = a->a1 != nullptr, scr = a->scratch != nullptr;
+  const dim3 grid(a->nblk), blk(NTHR);
+  if (saved && scr) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, true>), grid, blk, 0, (hipStream_t)stream, *a);
+  else if (saved) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, false>), grid, blk, 0, (hipStream_t)stream, *a);
+  else if (scr) hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true>), grid, blk, 0, (hipStream_t)stream, *a);
+  else hipLaunchKernelGGL((edge_bwd_fused_kernel<false, false>), grid, blk, 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

@@ -1281,9 +1281,6 @@ extern "C" int agn_debug_fwd_stamps(void* p) {
 #endif
 
 namespace agn {
-int edge16_fwd_set_halves(int nh);  // edge16_fwd.hip
-int edge16_fwd_set_waves(int nw);   // edge16_fwd.hip
-int edge32_fwd_set_option(int key, int value);  // edge32_fwd.hip
 bool node32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);  // node32_fwd.hip
 bool enc32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
 bool dec32_fwd_try(const agn_mlp_fwd_args* a, void* stream, int* rc);   // enc32_fwd.hip
@@ -1296,9 +1293,6 @@ extern "C" {
 int agn_version(void) { return 1; }
 
 int agn_set_option(int key, int value) {
-  if (key == AGN_OPT_EDGE_FWD_HALVES) return agn::edge16_fwd_set_halves(value);
-  if (key == AGN_OPT_EDGE_FWD_WAVES) return agn::edge16_fwd_set_waves(value);
-  if (key == AGN_OPT_EDGE_FWD32_WAVES || key == AGN_OPT_EDGE_FWD32_PRIO) return agn::edge32_fwd_set_option(key, value);
   if (key == AGN_OPT_RESIDENT) {
     const int old = g_opt_resident;
     g_opt_resident = value ? 1 : 0;

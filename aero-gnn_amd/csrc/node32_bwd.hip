@@ -385,8 +385,15 @@ int cu_count() {
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // per-tile LayerNorm partial workspace, grown on demand (device memory kept for the process)
-float* g_lnt = nullptr;
-size_t g_lnt_cap = 0;
+// LayerNorm partial-row workspace, one per device (a process driving two devices must not
+// share it); a call on another stream than the last user first waits for that stream, which may still
+// be reading it
+struct LnScratch {
+  float* p = nullptr;
+  size_t cap = 0;
+  hipStream_t last = nullptr;
+};
+LnScratch g_lnt[64];
 long g_launches = 0;
 long g_dec_launches = 0;
 
@@ -420,26 +427,33 @@ bool node32_bwd_try(const agn_mlp_bwd_args* a, void* stream, int* rc, int* ln_ro
   const int ntiles = (a->rows + 31) / 32;
   const int nblk = (ntiles + ROWS_PER_BLOCK / 32 - 1) / (ROWS_PER_BLOCK / 32);
   hipStream_t st = (hipStream_t)stream;
+  float* lnt = nullptr;
   if (a->ln_partial) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    LnScratch& w = g_lnt[dev & 63];
+    if (w.last && w.last != st && hipStreamSynchronize(w.last) != hipSuccess) return false;
     const size_t need = (size_t)ntiles * 2 * H;
-    if (need > g_lnt_cap) {
-      if (g_lnt) {
+    if (need > w.cap) {
+      if (w.p) {
         if (hipStreamSynchronize(st) != hipSuccess) return false;
-        (void)hipFree(g_lnt);
-        g_lnt = nullptr;
-        g_lnt_cap = 0;
+        (void)hipFree(w.p);
+        w.p = nullptr;
+        w.cap = 0;
       }
-      if (hipMalloc(&g_lnt, need * sizeof(float)) != hipSuccess) {
-        g_lnt = nullptr;
+      if (hipMalloc(&w.p, need * sizeof(float)) != hipSuccess) {
+        w.p = nullptr;
         return false;
       }
-      g_lnt_cap = need;
+      w.cap = need;
     }
+    w.last = st;
+    lnt = w.p;
   }
   const int grid = grid_for(ntiles);
-  hipLaunchKernelGGL(node32_bwd_kernel, dim3(grid), dim3(64 * NW), 0, st, *a, g_lnt);
+  hipLaunchKernelGGL(node32_bwd_kernel, dim3(grid), dim3(64 * NW), 0, st, *a, lnt);
   if (a->ln_partial)
-    hipLaunchKernelGGL(node32_lnp_kernel, dim3((nblk * 2 * H + 255) / 256), dim3(256), 0, st, g_lnt, ntiles, nblk,
+    hipLaunchKernelGGL(node32_lnp_kernel, dim3((nblk * 2 * H + 255) / 256), dim3(256), 0, st, lnt, ntiles, nblk,
                        a->ln_partial);
   ++g_launches;
   *ln_rows = nblk;

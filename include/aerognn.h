@@ -197,18 +197,9 @@ const char* agn_error_string(int code);
 /* Process-wide kernel-selection options (testing / A-B measurement). Returns the previous value
  * or AGN_E_ARG. AGN_OPT_RESIDENT: 1 (default) = persistent resident-weight kernels for the
  * large bf16 H=128 edge MLPs, 0 = always the general kernels (bitwise-identical outputs).
- * AGN_OPT_EDGE_FWD_HALVES: 16-row halves per wave of agn_edge_forward, 1 or 2 (default);
- * AGN_OPT_EDGE_FWD_WAVES: waves per CU of the two-halves variant, 12 (default) or 16 (bitwise-
- * identical outputs; agn_edge_fwd_blocks follows both).
- * AGN_OPT_EDGE_FWD32_WAVES: waves per CU of agn_edge_forward32, 12 (default) or 16 (bitwise-
- * identical outputs; agn_edge_fwd32_blocks follows it). AGN_OPT_EDGE_FWD32_PRIO: its static wave
- * priorities, 0 = none, 1 = the k-th wave of each SIMD at priority k, 2 = the reverse. */
+ * (Keys 1-4 selected measured-slower edge-forward variants, removed in round 6; rejected.) */
 enum {
-  AGN_OPT_RESIDENT = 0,
-  AGN_OPT_EDGE_FWD_HALVES = 1,
-  AGN_OPT_EDGE_FWD_WAVES = 2,
-  AGN_OPT_EDGE_FWD32_WAVES = 3,
-  AGN_OPT_EDGE_FWD32_PRIO = 4
+  AGN_OPT_RESIDENT = 0
 };
 int agn_set_option(int key, int value);
 /* bytes of a packed A operand with `m` rows and `k` reduction columns */
@@ -394,40 +385,40 @@ typedef struct {
   float* db_partial;         /* [3][nblk][128] */
   float* ln_partial;         /* [nblk][2][128]: sum g * xhat, sum g (LayerNorm weight / bias grads) */
   unsigned long long* stamps; /* diagnostics only (a -DAGN_EB_STAMPS build): NULL, or [2][8][8][16] */
-  /* optional (agn_edge_bwd_fused only; agn_edge_backward rejects a non-NULL dpd): dP_d, the
-   * receiver segment sums of G0, bitwise agn_segment_sum(nodes, 128, BF16, rowptr, NULL, g0, ..).
-   * The dW waves recompute their 32 features of G0 from each tile's L1 hand-off and sum the
-   * receiver runs that lie inside one 128-row round; a second launch on the same stream sums the
-   * receivers whose edges span a round boundary, and zeroes the empty ones. */
-  void* dpd;                 /* [nodes][128] out, or NULL */
-  const int32_t* rowptr;     /* [nodes + 1] receiver offsets of dst (dst sorted: CSC order) */
-  int nodes;                 /* < 2^24 */
+  /* the forward's saves (agn_edge_forward32 with act[0] / stats): a1 = relu(h0) in AGN_TILED and
+   * the LayerNorm (mean, rstd) [rows][2]. Given both, the kernel starts its recompute at Lin1 from
+   * a1 (bitwise the values it would recompute) and reads no e, proj or src; NULL = recompute h0. */
+  const void* a1;
+  const float* stats;
+  /* optional: [nblk][4][2][32][128] bf16 (64 KB per block, agn_edge_bwd_scratch_bytes), the chain
+   * waves' a2 / a3 parked between the recompute and their hand-offs (L2-resident: rewritten every
+   * tile). NULL = a2 / a3 recomputed a second time from a1. Outputs are bitwise the same. */
+  void* scratch;
+  /* packed A = W_e^T (agn_pack trans = 1, bf16): de = G0 W_e + S reads it from L2 (round 6: W_e's
+   * LDS image went to the hand-off ring) */
+  const void* wtpk0;
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
+size_t agn_edge_bwd_scratch_bytes(int nblk);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
 /* Device fault word of the persistent hand-off kernels (agn_edge_bwd_fused's LDS ring): the OR of
  * AGN_FAULT_* bits recorded since the last reset (0 = none). A set bit means a bounded wait gave
  * up and that launch's dW / db are wrong. Synchronises the device; reset != 0 clears the word. */
 #define AGN_FAULT_RING_TIMEOUT 1
 int agn_fault_status(int* value, int reset);
-/* The same words without a device synchronisation: enqueues on `stream` copies of the fault word
- * of agn_edge_bwd_fused (to host_pinned[0]) and of agn_edge_backward (host_pinned[1]) into
- * page-locked host memory; the values are valid once the stream reaches the copies. Nothing is
- * reset. The production path polls this once per step (aerognn/core.py). */
+/* The same word without a device synchronisation: enqueues on `stream` a copy of the fault word
+ * of agn_edge_bwd_fused into page-locked host memory (host_pinned[0]); the value is valid once
+ * the stream reaches the copy. Nothing is reset. The production path enqueues one every
+ * FAULT_POLL_EVERY (16) fused launches and reads it once its event has completed, and
+ * GradAllReduce / the optimizer-step hook drain the last one (aerognn/core.py). */
 int agn_fault_status_async(int* host_pinned, void* stream);
-/* ---- 16-row-tile sum-trick edge chain (bf16, H = 128; csrc/edge16*.hip) ----
- * The same EdgeBlockSum chain (mgnLayer.py:72-105, residual :205) on v_mfma_f32_16x16x32_bf16
- * 16-edge tiles: the forward keeps four waves per SIMD, and the fused backward two chain waves
- * per SIMD beside the dW accumulators. The backward's forward recompute is bitwise
- * agn_edge_forward's (shared k-order); the pair replaces agn_mlp_forward + agn_edge_bwd_fused
- * for these chains.
- *   agn_edge_forward : out = e + LN(chain(e, P_s[src] + P_d[dst])); act[0..2] (relu outputs
- *                      a1..a3), hpre (pre-LN row) and stats (mean, rstd) are optional row-major
- *                      saves for parity tests (NULL in production: the backward recomputes).
- *   agn_edge_backward: agn_edge_bwd_args as agn_edge_bwd_fused, grid agn_edge_backward_blocks. */
+/* testing: sets the fault word (as a ring wait that gave up would), so the host-side polling can be
+ * exercised without a real fault */
+int agn_debug_set_fault(int value);
+/* ---- arguments of the sum-trick edge chain's forward kernel (agn_edge_forward32) ---- */
 typedef struct {
   int rows;                  /* edges (CSC order) */
-  int nblk;                  /* grid size: agn_edge_fwd_blocks(rows) */
+  int nblk;                  /* grid size: agn_edge_fwd32_blocks(rows) */
   const void* wpk[4];        /* packed A = W_l of W_e, Lin1, Lin2, Lin3 (agn_pack trans = 0, bf16) */
   const float* bias[4];      /* fp32 biases; bias[1..3] of Lin1..Lin3 (bias[0] unused) */
   const float* ln_g;         /* LayerNorm gamma, beta [128] */
@@ -437,21 +428,18 @@ typedef struct {
   const int32_t* src;
   const int32_t* dst;
   void* out;                 /* [rows][128] e' */
-  void* act[3];              /* optional [rows][128] a1, a2, a3 */
-  void* hpre;                /* optional [rows][128] h3 (bf16) */
-  float* stats;              /* optional [rows][2] */
+  void* act[3];              /* training saves: act[0] = a1 in AGN_TILED (rows padded to 32); act[1..2] NULL */
+  void* hpre;                /* must be NULL */
+  float* stats;              /* training saves: [rows][2] LayerNorm (mean, rstd), or NULL */
 } agn_edge_fwd_args;
-int agn_edge_fwd_blocks(int rows);
-int agn_edge_forward(const agn_edge_fwd_args* a, void* stream);
-/* The same chain on 32-edge tiles with 32x32x16 MFMAs, bitwise agn_mlp_forward's resident kernel
- * on the same operands (so agn_edge_bwd_fused's recompute pairs with it): the forward of the
- * training step (fused backward) and of inference. No saves (act / hpre / stats must be NULL);
- * grid agn_edge_fwd32_blocks(rows). Replaces mlp.py:37-60 MLP.forward on EdgeBlockSum's chain
- * (mgnLayer.py:72-105) as agn_edge_forward does. */
+/* The chain on 32-edge tiles with 32x32x16 MFMAs, bitwise agn_mlp_forward's resident kernel
+ * on the same operands: the forward of the training step (fused backward) and of inference.
+ * Grid agn_edge_fwd32_blocks(rows). Replaces mlp.py:37-60 MLP.forward on EdgeBlockSum's chain
+ * (mgnLayer.py:72-105, residual :205). With act[0] and stats set (training) it also saves the
+ * first ReLU output a1 (AGN_TILED) and the LayerNorm statistics, which agn_edge_bwd_fused reads
+ * instead of recomputing h0 from e and the projection rows. */
 int agn_edge_fwd32_blocks(int rows);
 int agn_edge_forward32(const agn_edge_fwd_args* a, void* stream);
-int agn_edge_backward_blocks(int rows);
-int agn_edge_backward(const agn_edge_bwd_args* a, void* stream);
 /* dw[m][k] = sum_s dw_partial[s][m][k] (and db) for each desc: the fixed-order second stage
  * of agn_wgrad on caller-provided slabs (m, k <= 128 per desc here) */
 int agn_wgrad_reduce(const agn_wgrad_batch* b, int nsplit, void* stream);

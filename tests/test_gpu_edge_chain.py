@@ -1,0 +1,344 @@
+"""The fused sum-trick edge chain: agn_edge_forward32 (csrc/edge32_fwd.hip) and agn_edge_bwd_fused
+(csrc/edge_bwd.hip), the bf16 H = 128 training pair, against a mask-matched float64 backward.
+
+Reference chain: models/mgnLayer.py:72-105 (EdgeBlockSum) and the residual of :205, under autograd.
+The kernels compute in bf16 with fp32 accumulation. The tests remove every source of difference
+except the kernels' own roundings:
+
+* backward, mask-matched: the float64 backward runs through the kernel's own ReLU masks and saved
+  bf16 activations (the forward's, which the fused backward recomputes bitwise), so no ReLU kink
+  flips between the two sides; what remains is the kernel's bf16 rounding of each G_L (~1e-3 per
+  rounding). Every output (de, G0, dW1..dW3, db1..db3, the LayerNorm partials) is gated at 3x its
+  measured rel-L2.
+* the backward's variants (its recompute started from the forward's a1 / statistics or from e and
+  the projection rows; a2 / a3 parked in the L2 scratch or recomputed) are bitwise one another.
+"""
+import os
+
+import pytest
+import torch
+
+from golden_util import rel_l2
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("AEROGNN_MEMLOG", "0")
+DEV = "cuda"
+H = 128
+
+# worst rel-L2 over the parametrised cases, measured on the MI355X (profiles/r5_gpu_edge16_tests.log,
+# both round-5 kernels identical to 3 digits); each gate is 3x. The float64 side does not round G_L to
+# bf16, the kernel does (~1e-3 per rounding, accumulating down the chain); the LayerNorm partials are
+# fp32 sums of fp32 products (~1e-7).
+BWD_MEASURED = {"de": 2.41e-3, "g0": 3.36e-3, "dW1": 2.75e-3, "dW2": 2.32e-3, "dW3": 1.58e-3, "db1": 2.71e-3,
+                "db2": 2.34e-3, "db3": 1.59e-3, "dgamma": 1.6e-7, "dbeta": 1.5e-7}
+
+# (saved, scratch): the backward's recompute from the forward's a1 / statistics, a2 / a3 through the scratch
+VARIANTS = {"saved_scratch": (True, True), "saved": (True, False), "recompute_scratch": (False, True),
+            "recompute": (False, False)}
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+class Chain:
+    """Random fp32 master parameters of one EdgeBlockSum chain (W_e, 3 Linears, LayerNorm), packed
+    as the model packs them (aerognn.functions.ChainSpec)."""
+
+    def __init__(self, seed):
+        from aerognn.core import Pack
+        from aerognn.functions import ChainSpec
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        s = H ** -0.5
+        self.we = (torch.randn(H, H, generator=g) * s).to(DEV)
+        self.w = [(torch.randn(H, H, generator=g) * s).to(DEV) for _ in range(3)]
+        self.b = [(torch.randn(H, generator=g) * 0.1).to(DEV) for _ in range(3)]
+        self.gamma = (1.0 + 0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.beta = (0.1 * torch.randn(H, generator=g)).to(DEV)
+        self.pack = Pack()
+        self.spec = ChainSpec([(self.we, None)] + list(zip(self.w, self.b)), (self.gamma, self.beta), H, self.pack, "e")
+        self.pack.update(torch.bfloat16, torch.device(DEV))
+
+
+def _level(N, E, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.to(torch.int32)
+    src = torch.randint(0, N, (E,), generator=g).to(torch.int32)
+    return src.to(DEV), dst.to(DEV)
+
+
+def _inputs(N, E, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed + 1)
+    e = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    P = torch.randn(N, 2 * H, generator=g).to(torch.bfloat16).to(DEV)
+    gi = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    g2 = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    return e, P, gi, g2
+
+
+def _bwd_ref(ch, e, P, src, dst, gi, g2, acts, hpre, stats):
+    """float64 backward of the chain through the kernel's own masks and saved bf16 activations."""
+    a1, a2, a3 = (t.double() for t in acts)
+    we, w = _bf(ch.we), [_bf(x) for x in ch.w]
+    S = (gi.double() if gi is not None else 0.0) + g2.double()[dst.long()]
+    mean, rstd = stats[:, 0].double(), stats[:, 1].double()
+    xh = (hpre.double() - mean[:, None]) * rstd[:, None]
+    gg = S * ch.gamma.double()
+    c1 = gg.mean(1, keepdim=True)
+    c2 = (gg * xh).mean(1, keepdim=True)
+    G3 = (gg - c1 - xh * c2) * rstd[:, None]
+    out = {"dgamma": (S * xh).sum(0), "dbeta": S.sum(0), "dW3": G3.T @ a3, "db3": G3.sum(0)}
+    G2 = (G3 @ w[2]) * (a3 > 0)
+    out["dW2"], out["db2"] = G2.T @ a2, G2.sum(0)
+    G1 = (G2 @ w[1]) * (a2 > 0)
+    out["dW1"], out["db1"] = G1.T @ a1, G1.sum(0)
+    G0 = (G1 @ w[0]) * (a1 > 0)
+    out["g0"] = G0
+    out["de"] = G0 @ we + S
+    return out
+
+
+def _fwd_saves(ch, e, P, src, dst):
+    """agn_edge_forward32 with its training saves (a1 AGN_TILED, LayerNorm statistics)."""
+    from aerognn import core
+    E = e.shape[0]
+    out = torch.empty_like(e)
+    a1 = core.tiled_empty(E, H, torch.bfloat16, e.device)
+    st = torch.empty(E, 2, dtype=torch.float32, device=DEV)
+    core.edge_forward(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P, src=src,
+                      dst=dst, out=out, a1=a1, stats=st)
+    return out, a1, st
+
+
+def _backward(ch, e, P, src, dst, gi, g2, variant="saved_scratch"):
+    from aerognn import core
+    from aerognn.core import colsum_rows
+    saved, scratch = VARIANTS[variant]
+    E = e.shape[0]
+    a1 = st = None
+    if saved:
+        _, a1, st = _fwd_saves(ch, e, P, src, dst)
+    de, g0 = torch.empty_like(e), torch.empty_like(e)
+    dw, db, part, nb = core.edge_bwd_fused(rows=E, wpk=ch.spec.wpk(), wtpk0=ch.spec.wtpk()[0], bias=ch.spec.biases(), ln_g=ch.spec.lnp()[0],
+                                           e=None if saved else e, proj=None if saved else P,
+                                           src=None if saved else src, dst=dst, g=gi, g2=g2, de=de, g0=g0,
+                                           a1=a1, stats=st, scratch=scratch)
+    ln = torch.empty(2 * H, dtype=torch.float32, device=DEV)
+    colsum_rows(part, nb, 2 * H, ln)
+    got = {"de": de, "g0": g0, "dgamma": ln[:H], "dbeta": ln[H:], "part": part}
+    for l in range(3):
+        got[f"dW{l + 1}"], got[f"db{l + 1}"] = dw[l], db[l]
+    return got
+
+
+def _decode_tiled(t, rows):
+    """AGN_TILED [rows_pad, 128] bf16 -> row-major [rows, 128] (aerognn.h: unit (i, h) of row c holds
+    features 16i+4h+{0..3}, 16i+8+4h+{0..3})."""
+    u = t.view(torch.int16).reshape(-1, 8, 2, 32, 8)  # [tile][i][h][c][8]
+    out = torch.empty(u.shape[0], 32, H, dtype=torch.int16, device=t.device)
+    for i in range(8):
+        for hh in range(2):
+            v = u[:, i, hh]
+            out[:, :, 16 * i + 4 * hh:16 * i + 4 * hh + 4] = v[:, :, :4]
+            out[:, :, 16 * i + 8 + 4 * hh:16 * i + 8 + 4 * hh + 4] = v[:, :, 4:]
+    return out.reshape(-1, H)[:rows].view(torch.bfloat16)
+
+
+def _forward_32(ch, e, P, src, dst, decode=True):
+    """The 32-row resident forward (agn_mlp_forward) with the split path's saves (AGN_TILED): the
+    activations the 32-row fused backward recomputes bitwise."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves
+    E = e.shape[0]
+    out = torch.empty_like(e)
+    acts, hpre, stats = _alloc_saves(ch.spec, E, torch.bfloat16, torch.device(DEV), True)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     ln=ch.spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=out, acts=acts, hpre=hpre, stats=stats)
+    if not decode:
+        return out, acts, hpre, stats
+    return out, [_decode_tiled(a, E) for a in acts], _decode_tiled(hpre, E), stats
+
+
+@pytest.mark.parametrize("variant", ["saved_scratch", "recompute"])
+@pytest.mark.parametrize("N,E,with_g", [(5000, 70001, True), (100000, 598400, True), (300, 17, True),
+                                        (20000, 100000, False)])
+def test_edge_backward_mask_matched_fp64(variant, N, E, with_g):
+    """the fused backward against the float64 backward run through the kernel's
+    own ReLU masks and bf16 saves (the forward whose recompute the kernel reproduces bitwise)."""
+    ch = Chain(5)
+    src, dst = _level(N, E, 6)
+    e, P, gi, g2 = _inputs(N, E, 7)
+    if not with_g:
+        gi = None
+    _, acts, hpre, stats = _forward_32(ch, e, P, src, dst)
+    got = _backward(ch, e, P, src, dst, gi, g2, variant)
+    torch.cuda.synchronize()
+    ref = _bwd_ref(ch, e, P, src, dst, gi, g2, acts, hpre, stats)
+    fails = []
+    for k, v in ref.items():
+        r = rel_l2(got[k].double(), v)
+        gate = 3.0 * BWD_MEASURED[k]
+        print(f"fused backward [{variant}] E={E} {k}: rel-L2 {r:.3e} against the mask-matched float64 backward "
+              f"(gate {gate:.1e})")
+        if not r <= gate:
+            fails.append((k, r))
+    assert not fails, fails
+
+
+@pytest.mark.parametrize("N,E,with_g", [(5000, 70001, True), (300, 17, True), (20000, 100000, False),
+                                        (100000, 598400, True)])
+def test_fused_backward_variants_bitwise(N, E, with_g):
+    """Round 6: the recompute started from the forward's a1 / statistics and a2 / a3 read back from
+    the L2 scratch give the round-5 kernel's outputs bit for bit (de, G0, dW, db, LayerNorm partials):
+    the same operands reach the same MFMA and VALU sequences."""
+    ch = Chain(31)
+    src, dst = _level(N, E, 32)
+    e, P, gi, g2 = _inputs(N, E, 33)
+    if not with_g:
+        gi = None
+    runs = {v: _backward(ch, e, P, src, dst, gi, g2, v) for v in VARIANTS}
+    torch.cuda.synchronize()
+    base = runs["recompute"]
+    for v, got in runs.items():
+        for k in base:
+            assert torch.equal(got[k].view(torch.int16) if got[k].dtype == torch.bfloat16 else got[k],
+                               base[k].view(torch.int16) if base[k].dtype == torch.bfloat16 else base[k]), (v, k)
+    from aerognn import _lib as L
+    assert L.fault_status(reset=True) == 0
+
+
+@pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (64, 32), (1000, 96)])
+def test_edge32_forward_saves(N, E):
+    """agn_edge_forward32's training saves: a1 equals the resident kernel's AGN_TILED a1 save and the
+    statistics its stats save, bitwise; the output is the same with and without saves."""
+    from aerognn import core
+    ch = Chain(41)
+    src, dst = _level(N, E, 42)
+    e, P, _, _ = _inputs(N, E, 43)
+    out_ref, acts, _, stats = _forward_32(ch, e, P, src, dst, decode=False)
+    out, a1, st = _fwd_saves(ch, e, P, src, dst)
+    plain = torch.empty_like(e)
+    core.edge_forward(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P, src=src,
+                      dst=dst, out=plain)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int16), out_ref.view(torch.int16))
+    assert torch.equal(plain.view(torch.int16), out_ref.view(torch.int16))
+    n = (E + 31) // 32 * 32
+    # rows past E in the last tile are padding (not written by either kernel)
+    assert torch.equal(_decode_tiled(a1, E).view(torch.int16), _decode_tiled(acts[0], E).view(torch.int16))
+    assert torch.equal(st, stats)
+    assert a1.shape[0] == n
+
+
+def test_fused_backward_deterministic():
+    """Two launches give bitwise-equal outputs (fixed-order sums everywhere, no float atomics)."""
+    N, E = 20000, 130001
+    ch = Chain(9)
+    src, dst = _level(N, E, 10)
+    e, P, gi, g2 = _inputs(N, E, 11)
+    a = _backward(ch, e, P, src, dst, gi, g2)
+    b = _backward(ch, e, P, src, dst, gi, g2)
+    torch.cuda.synchronize()
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("N,E", [(5000, 70001), (300, 17), (40000, 240000), (64, 32), (1000, 96)])
+def test_edge32_forward_bitwise_resident(N, E):
+    """agn_edge_forward32 (csrc/edge32_fwd.hip) against agn_mlp_forward's
+    resident kernel on the same operands: bitwise (the same MFMA sequence per accumulator, the same
+    exact row sum and LayerNorm steps), which is what lets the 32-row fused backward's recompute
+    pair with it. Ragged tails (E % 32 != 0) and a single tile included."""
+    from aerognn import core
+    from aerognn import _lib as L
+    ch = Chain(21)
+    src, dst = _level(N, E, 22)
+    e, P, _, _ = _inputs(N, E, 23)
+    ref = torch.empty_like(e)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     ln=ch.spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=ref)
+    out = torch.full_like(e, float("nan"))
+    core.edge_forward(rows=E, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P,
+                      src=src, dst=dst, out=out)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(ref.float()).all())
+    assert torch.equal(out, ref)
+
+
+def test_edge32_forward_rejects_bad_saves():
+    """Only a1 and the statistics can be saved, both or neither (aerognn.h agn_edge_fwd_args)."""
+    from aerognn import core
+    from aerognn import _lib as L
+    import ctypes as C
+    ch = Chain(24)
+    src, dst = _level(100, 300, 25)
+    e, P, _, _ = _inputs(100, 300, 26)
+    with pytest.raises(L.AeroGNNError):  # a1 without the statistics
+        core.edge_forward(rows=300, wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), e=e, proj=P, src=src,
+                          dst=dst, out=torch.empty_like(e), a1=core.tiled_empty(300, H, torch.bfloat16, e.device))
+    a = L.EdgeFwdArgs()
+    a.rows, a.nblk = 300, int(L.lib().agn_edge_fwd32_blocks(300))
+    for i in range(4):
+        a.wpk[i] = ch.spec.wpk()[i]
+        a.bias[i] = ch.spec.biases()[i]
+    a.ln_g, a.ln_b = ch.spec.lnp()
+    h = torch.empty_like(e)
+    a.e, a.proj, a.src, a.dst, a.out, a.hpre = e.data_ptr(), P.data_ptr(), src.data_ptr(), dst.data_ptr(), h.data_ptr(), h.data_ptr()
+    assert L.lib().agn_edge_forward32(C.byref(a), core.stream()) != 0  # hpre is not a save of this kernel
+
+
+def test_fault_status_async_reads_words():
+    """agn_fault_status_async (the production path's poll, aerognn/core.py _poll_faults): copies
+    both fused backwards' fault words to page-locked host memory without a device sync."""
+    import ctypes as C
+    from aerognn import _lib as L
+    from aerognn import core
+    assert L.fault_status(reset=True) == 0
+    buf = torch.full((2,), -1, dtype=torch.int32, pin_memory=True)
+    core.check(L.lib().agn_fault_status_async(C.c_void_p(buf.data_ptr()), core.stream()), "fault_status_async")
+    torch.cuda.synchronize()
+    assert buf.tolist() == [0, -1]  # one word
+    # the poll itself: FAULT_POLL_EVERY calls enqueue one copy, a later call reads it
+    old = core.FAULT_POLL_EVERY
+    core.FAULT_POLL_EVERY = 1
+    try:
+        core._poll_faults()
+        torch.cuda.synchronize()
+        core._poll_faults()
+    finally:
+        core.FAULT_POLL_EVERY = old
+
+
+def test_fault_checkpoint_reads_the_last_launch():
+    """a fault word set by the LAST fused launch of a run (fewer than
+    FAULT_POLL_EVERY launches since the previous copy) is still read: the optimizer-step pre-hook
+    enqueues a copy covering it and fault_checkpoint(block=True) (also the atexit check) raises."""
+    from aerognn import core
+    from aerognn import _lib as L
+    assert L.fault_status(reset=True) == 0
+    old = core.CHECK_FAULTS
+    core.CHECK_FAULTS = False
+    core._fault.update(event=None, n=0, dirty=False)
+    try:
+        ch = Chain(51)
+        src, dst = _level(3000, 70001, 52)
+        e, P, gi, g2 = _inputs(3000, 70001, 53)
+        _backward(ch, e, P, src, dst, gi, g2, "recompute")
+        torch.cuda.synchronize()
+        core.fault_checkpoint(block=True)  # a clean launch: no fault
+        assert L.lib().agn_debug_set_fault(1) == 0  # as a ring wait that gave up in the next launch would
+        _backward(ch, e, P, src, dst, gi, g2, "recompute")
+        assert core._fault["dirty"] and core._fault["n"] < core.FAULT_POLL_EVERY
+        p = torch.zeros(4, device=DEV, requires_grad=True)
+        p.grad = torch.ones_like(p)
+        opt = torch.optim.SGD([p], lr=0.1)
+        with pytest.raises(L.AeroGNNError):
+            opt.step()  # the pre-hook enqueues the copy (it raises here only if the copy already landed)
+            core.fault_checkpoint(block=True)
+    finally:
+        L.fault_status(reset=True)
+        core._fault.update(event=None, n=0, dirty=False)
+        core.CHECK_FAULTS = old

@@ -1,0 +1,295 @@
+"""The bf16 node-side chain kernels against mask-matched float64 references:
+the processor layer's node MLP (node32_fwd_kernel with its receiver walk, node32_bwd_kernel, and the
+weight gradients agn_wgrad forms from its G saves), the decoder (dec32_fwd / dec32_bwd) and the
+encoders (enc32_fwd and the encoder backward), plus the edge chain's forward layer by layer.
+
+The float64 side runs each layer from the kernel's own saved bf16 activations and backpropagates
+through the kernel's own ReLU masks (tests/maskmatched.py), so the remaining difference is the
+kernel's bf16 rounding of each G_l: every backward output is gated at 3x its measured rel-L2.
+Reference: models/mgnLayer.py:134-153 (NodeBlock + residual), :211, models/mlp.py:40-51,
+models/bsms_mgn.py:138-139 (encoders) and the decoder.
+"""
+import os
+
+import pytest
+import torch
+
+from golden_util import rel_l2
+from maskmatched import H, bf, chain_backward_ref, chain_forward_check, gate, rows_of
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("AEROGNN_MEMLOG", "0")
+DEV = "cuda"
+
+# worst measured rel-L2 over each test's cases on the MI355X (profiles/r6_gpu_mask_matched.log);
+# gates are 3x
+NODE_MEASURED = {"G3": 1.66e-3, "G2": 2.36e-3, "G1": 2.90e-3, "G0": 3.35e-3, "dx": 2.10e-3, "dagg": 3.74e-3,
+                 "dW0": 3.38e-3, "db0": 4.42e-3, "dW1": 3.10e-3, "db1": 3.56e-3, "dW2": 2.53e-3, "db2": 2.80e-3,
+                 "dW3": 1.74e-3, "db3": 1.85e-3, "dgamma": 1.82e-7, "dbeta": 1.10e-7}
+# the decoder's by depth from its output layer (d = 0: G = the incoming gradient itself, exact)
+DEC_MEASURED_BY_DEPTH = [{"G": 1e-7, "dW": 1.76e-7, "db": 1.09e-7}, {"G": 1.66e-3, "dW": 1.85e-3, "db": 2.06e-3},
+                         {"G": 2.34e-3, "dW": 2.50e-3, "db": 2.58e-3}, {"G": 2.88e-3, "dW": 2.94e-3, "db": 3.54e-3}]
+DEC_MEASURED_DX = 3.31e-3
+ENC_MEASURED = {"G2": 1.66e-3, "G1": 2.36e-3, "G0": 2.90e-3, "dx": 3.65e-3, "dW0": 2.84e-3, "db0": 3.14e-3,
+                "dW1": 2.32e-3, "db1": 2.27e-3, "dW2": 1.74e-3, "db2": 1.86e-3, "dgamma": 1.95e-7, "dbeta": 1.49e-7}
+
+
+class Chain:
+    """Random fp32 master parameters of one MLP chain, packed as the model packs them."""
+
+    def __init__(self, seed, dims, ln, prefix):
+        from aerognn.core import Pack
+        from aerognn.functions import ChainSpec
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        self.w = [(torch.randn(o, i, generator=g) * i ** -0.5).to(DEV) for i, o in zip(dims[:-1], dims[1:])]
+        self.b = [(torch.randn(o, generator=g) * 0.1).to(DEV) for o in dims[1:]]
+        self.ln = None
+        if ln:
+            self.ln = ((1.0 + 0.1 * torch.randn(dims[-1], generator=g)).to(DEV), (0.1 * torch.randn(dims[-1], generator=g)).to(DEV))
+        self.pack = Pack()
+        self.spec = ChainSpec(list(zip(self.w, self.b)), self.ln, H, self.pack, prefix)
+        self.pack.update(torch.bfloat16, torch.device(DEV))
+        self.W64 = [bf(w) for w in self.w]
+        self.b64 = [b.double() for b in self.b]
+        self.ln64 = None if self.ln is None else tuple(t.double() for t in self.ln)
+
+
+def _counter(name):
+    from aerognn import _lib as L
+    return int(getattr(L.lib(), name)())
+
+
+def _param_grads(ch, gpre, inputs0, acts, part, nb):
+    from aerognn.functions import _chain_param_grads
+    gr = _chain_param_grads(ch.spec, gpre, inputs0, acts, part, nb)
+    out = {}
+    for l in range(len(ch.w)):
+        out[f"dW{l}"], out[f"db{l}"] = gr[2 * l], gr[2 * l + 1]
+    if ch.ln is not None:
+        out["dgamma"], out["dbeta"] = gr[-2], gr[-1]
+    return out
+
+
+def _graph(N, E, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values
+    rowptr = torch.zeros(N + 1, dtype=torch.int64)
+    rowptr[1:] = torch.cumsum(torch.bincount(dst, minlength=N), 0)
+    return dst.to(DEV), rowptr.to(torch.int32).to(DEV)
+
+
+@pytest.mark.parametrize("N,E", [(100000, 598400), (65601, 393606)])
+def test_node_chain_mask_matched_fp64(N, E):
+    """node32_fwd (receiver SUM walk, training saves) -> node32_bwd -> agn_wgrad, the processor
+    layer's NodeBlock at C2 size and at a ragged size (partial last tile and 128-row block)."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves, _alloc_gpre
+    ch = Chain(61, [2 * H, H, H, H, H], True, "n")
+    dst, rowptr = _graph(N, E, 62)
+    g = torch.Generator(device="cpu").manual_seed(63)
+    x = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    ep = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    gx = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    acts, hpre, stats = _alloc_saves(ch.spec, N, torch.bfloat16, x.device, True)
+    out = torch.empty_like(x)
+    agg = torch.empty_like(x)
+    n0 = _counter("agn_debug_node32_launches")
+    core.mlp_forward(rows=N, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None), (L.SEG_SUM, H, ep.stride(0), ep, rowptr, agg)],
+                     wpk=ch.spec.wpk(), bias=ch.spec.biases(), ln=ch.spec.lnp(), resid=x, out=out,
+                     acts=acts, hpre=hpre, stats=stats)
+    gpre = _alloc_gpre(ch.spec, N, torch.bfloat16, x.device)
+    dx, dagg = torch.empty_like(x), torch.empty_like(x)
+    part = torch.empty(core.bwd_nblocks(N), 2 * H, dtype=torch.float32, device=DEV)
+    nb0 = _counter("agn_debug_node32_bwd_launches")
+    nb = core.mlp_backward(rows=N, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H, in_dim=2 * H,
+                           wtpk=ch.spec.wtpk(), acts=acts, g=gx, gpre=gpre, ln_g=ch.spec.lnp()[0], hpre=hpre,
+                           stats=stats, din=[(H, dx, True), (H, dagg, False)], ln_partial=part)
+    got = _param_grads(ch, gpre, [x, agg], acts, part, nb)
+    torch.cuda.synchronize()
+    # the resident kernels ran (not the general ones)
+    assert _counter("agn_debug_node32_launches") == n0 + 1
+    assert _counter("agn_debug_node32_bwd_launches") == nb0 + 1
+    A = [rows_of(a, N) for a in acts]
+    hp = rows_of(hpre, N)
+    # forward: the receiver sums (fp32 in edge order, rounded once), then layer by layer
+    agg64 = torch.zeros(N, H, dtype=torch.float64, device=DEV).index_add_(0, dst, ep.double())
+    from maskmatched import check_bf16_layer
+    print(f"node chain N={N} E={E}:")
+    check_bf16_layer("agg", agg, agg64, False)
+    X = torch.cat([x.double(), agg.double()], 1)
+    chain_forward_check(X, ch.W64, ch.b64, A, hp, stats, ch.ln64, out=out, resid=x.double())
+    ref = chain_backward_ref(X, ch.W64, A, gx.double(), ch.ln64, hp, stats)
+    res = {f"G{l}": rel_l2(rows_of(gpre[l], N).double(), ref[f"G{l}"]) for l in range(4)}
+    res["dx"] = rel_l2(dx.double(), ref["dX"][:, :H] + gx.double())
+    res["dagg"] = rel_l2(dagg.double(), ref["dX"][:, H:])
+    for k in ("dW0", "db0", "dW1", "db1", "dW2", "db2", "dW3", "db3", "dgamma", "dbeta"):
+        res[k] = rel_l2(got[k].double(), ref[k])
+    gate(res, NODE_MEASURED, "node chain")
+
+
+@pytest.mark.parametrize("N,nlin,out_dim", [(100000, 3, 3), (65601, 4, 7)])
+def test_decoder_mask_matched_fp64(N, nlin, out_dim):
+    """dec32_fwd (training saves) -> dec32_bwd -> agn_wgrad: the decoder MLP from H-wide rows to a few
+    outputs, no LayerNorm (models/bsms_mgn.py decoder, mlp.py:40-51)."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves, _alloc_gpre
+    ch = Chain(71 + nlin, [H] + [H] * (nlin - 1) + [out_dim], False, "d")
+    g = torch.Generator(device="cpu").manual_seed(72)
+    x = torch.randn(N, H, generator=g).to(torch.bfloat16).to(DEV)
+    gy = torch.randn(N, out_dim, generator=g).to(torch.bfloat16).to(DEV)
+    acts, _, _ = _alloc_saves(ch.spec, N, torch.bfloat16, x.device, True)
+    out = torch.empty(N, out_dim, dtype=torch.bfloat16, device=DEV)
+    n0 = _counter("agn_debug_dec32_launches")
+    core.mlp_forward(rows=N, dtype=torch.bfloat16, hidden=H, nlin=nlin, out_dim=out_dim,
+                     segs=[(L.SEG_PLAIN, H, x.stride(0), x, None, None)], wpk=ch.spec.wpk(), bias=ch.spec.biases(),
+                     out=out, acts=acts)
+    gpre = _alloc_gpre(ch.spec, N, torch.bfloat16, x.device)
+    dx = torch.empty_like(x)
+    nb0 = _counter("agn_debug_dec32_bwd_launches")
+    nb = core.mlp_backward(rows=N, dtype=torch.bfloat16, hidden=H, nlin=nlin, out_dim=out_dim, in_dim=H,
+                           wtpk=ch.spec.wtpk(), acts=acts, g=gy, gpre=gpre, din=[(H, dx, False)])
+    got = _param_grads(ch, gpre, x, acts, None, nb)
+    torch.cuda.synchronize()
+    assert _counter("agn_debug_dec32_launches") == n0 + 1
+    assert _counter("agn_debug_dec32_bwd_launches") == nb0 + 1
+    A = [rows_of(a, N) for a in acts]
+    print(f"decoder N={N} nlin={nlin} out={out_dim}:")
+    chain_forward_check(x.double(), ch.W64, ch.b64, A, None, None, None, out=out)
+    ref = chain_backward_ref(x.double(), ch.W64, A, gy.double())
+    res = {f"G{l}": rel_l2(rows_of(gpre[l], N).double(), ref[f"G{l}"]) for l in range(nlin)}
+    res["dx"] = rel_l2(dx.double(), ref["dX"])
+    for l in range(nlin):
+        res[f"dW{l}"] = rel_l2(got[f"dW{l}"].double(), ref[f"dW{l}"])
+        res[f"db{l}"] = rel_l2(got[f"db{l}"].double(), ref[f"db{l}"])
+    meas = {"dx": DEC_MEASURED_DX}
+    for l in range(nlin):
+        m = DEC_MEASURED_BY_DEPTH[nlin - 1 - l]
+        meas[f"G{l}"], meas[f"dW{l}"], meas[f"db{l}"] = m["G"], m["dW"], m["db"]
+    gate(res, meas, "decoder")
+
+
+@pytest.mark.parametrize("rows,k,gather", [(598400, 4, True), (65601, 6, False)])
+def test_encoder_mask_matched_fp64(rows, k, gather):
+    """enc32_fwd (training saves, PLAIN or GATHER rows of <= 16 features) -> the encoder backward ->
+    agn_wgrad: the node / edge encoders (models/bsms_mgn.py:138-139, the edge one reading edge_attr
+    through the level-0 permutation)."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves, _alloc_gpre
+    ch = Chain(81, [k, H, H, H], True, "x")
+    g = torch.Generator(device="cpu").manual_seed(82)
+    n_in = rows + 77
+    xin = torch.randn(n_in, k, generator=g).to(torch.bfloat16).to(DEV)
+    idx = torch.randperm(n_in, generator=g)[:rows].to(torch.int32).to(DEV) if gather else None
+    if not gather:
+        xin = xin[:rows].contiguous()
+    gy = torch.randn(rows, H, generator=g).to(torch.bfloat16).to(DEV)
+    acts, hpre, stats = _alloc_saves(ch.spec, rows, torch.bfloat16, xin.device, True)
+    out = torch.empty(rows, H, dtype=torch.bfloat16, device=DEV)
+    seg = (L.SEG_PLAIN, k, xin.stride(0), xin, None, None) if idx is None else \
+        (L.SEG_GATHER, k, xin.stride(0), xin, idx, None)
+    n0 = _counter("agn_debug_enc32_launches")
+    core.mlp_forward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=3, out_dim=H, segs=[seg], wpk=ch.spec.wpk(),
+                     bias=ch.spec.biases(), ln=ch.spec.lnp(), out=out, acts=acts, hpre=hpre, stats=stats)
+    gpre = _alloc_gpre(ch.spec, rows, torch.bfloat16, xin.device)
+    dxr = torch.empty(rows, k, dtype=torch.bfloat16, device=DEV)
+    part = torch.empty(core.bwd_nblocks(rows), 2 * H, dtype=torch.float32, device=DEV)
+    nb = core.mlp_backward(rows=rows, dtype=torch.bfloat16, hidden=H, nlin=3, out_dim=H, in_dim=k,
+                           wtpk=ch.spec.wtpk(), acts=acts, g=gy, gpre=gpre, ln_g=ch.spec.lnp()[0], hpre=hpre,
+                           stats=stats, din=[(k, dxr, False)], ln_partial=part)
+    got = _param_grads(ch, gpre, xin if idx is None else [(xin, idx)], acts, part, nb)
+    torch.cuda.synchronize()
+    assert _counter("agn_debug_enc32_launches") == n0 + 1
+    X = (xin if idx is None else xin[idx.long()]).double()
+    A = [rows_of(a, rows) for a in acts]
+    hp = rows_of(hpre, rows)
+    print(f"encoder rows={rows} k={k} gather={gather}:")
+    chain_forward_check(X, ch.W64, ch.b64, A, hp, stats, ch.ln64, out=out)
+    ref = chain_backward_ref(X, ch.W64, A, gy.double(), ch.ln64, hp, stats)
+    res = {f"G{l}": rel_l2(rows_of(gpre[l], rows).double(), ref[f"G{l}"]) for l in range(3)}
+    res["dx"] = rel_l2(dxr.double(), ref["dX"])
+    for key in ("dW0", "db0", "dW1", "db1", "dW2", "db2", "dgamma", "dbeta"):
+        res[key] = rel_l2(got[key].double(), ref[key])
+    gate(res, ENC_MEASURED, "encoder")
+
+
+@pytest.mark.parametrize("N,E", [(100000, 598400), (5000, 70001), (300, 17)])
+def test_edge_chain_forward_layers_fp64(N, E):
+    """The bf16 edge chain's forward (the 32-row kernels' arithmetic: agn_edge_forward32 is bitwise
+    the resident agn_mlp_forward kernel, tests/test_gpu_edge_chain.py) layer by layer against float64
+    from its own saves: h0 = e W_e^T + P_s[src] + P_d[dst], a1..a3, h3, LayerNorm statistics, e'."""
+    from aerognn import core
+    from aerognn import _lib as L
+    from aerognn.functions import _alloc_saves
+    ch = Chain(91, [H, H, H, H, H], True, "e")
+    g = torch.Generator(device="cpu").manual_seed(92)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.to(torch.int32).to(DEV)
+    src = torch.randint(0, N, (E,), generator=g).to(torch.int32).to(DEV)
+    e = torch.randn(E, H, generator=g).to(torch.bfloat16).to(DEV)
+    P = torch.randn(N, 2 * H, generator=g).to(torch.bfloat16).to(DEV)
+    from aerognn.functions import ChainSpec
+    from aerognn.core import Pack
+    pack = Pack()
+    spec = ChainSpec([(ch.w[0], None)] + list(zip(ch.w[1:], ch.b[1:])), ch.ln, H, pack, "e")
+    pack.update(torch.bfloat16, torch.device(DEV))
+    acts, hpre, stats = _alloc_saves(spec, E, torch.bfloat16, e.device, True)
+    out = torch.empty_like(e)
+    core.mlp_forward(rows=E, dtype=torch.bfloat16, hidden=H, nlin=4, out_dim=H,
+                     segs=[(L.SEG_PLAIN, H, e.stride(0), e, None, None)], wpk=spec.wpk(), bias=spec.biases(),
+                     ln=spec.lnp(), proj=P, src=src, dst=dst, resid=e, out=out, acts=acts, hpre=hpre, stats=stats)
+    torch.cuda.synchronize()
+    A = [rows_of(a, E) for a in acts]
+    hp = rows_of(hpre, E)
+    P64 = P.double()
+    h0_add = P64[src.long(), :H] + P64[dst.long(), H:]
+    print(f"edge chain N={N} E={E}:")
+    # layer 0 has no bias; the projection rows are its additive term
+    b64 = [h0_add] + ch.b64[1:]
+    chain_forward_check(e.double(), ch.W64, b64, A, hp, stats, ch.ln64, out=out, resid=e.double())
+
+
+@pytest.mark.parametrize("kind", ["hidden", "node", "decoder"])
+def test_gelu_chain_at_resident_sizes(kind):
+    """non-ReLU chains at >= 64K rows, where the resident kernels (node32 / enc32 / dec32 /
+    the resident edge MLP) must decline (each has an act_fn != RELU guard) and the general kernels
+    with their saved pre-activations take over: the launch counters of the resident kernels do not
+    move, and forward and gradients match a float64 autograd run of the same chain (mlp.py:40-51,
+    F.gelu exact) on the bf16-rounded inputs and weights."""
+    from models.mlp import MLP
+    N = 70001
+    dims = {"hidden": (H, H, 2, True), "node": (2 * H, H, 2, True), "decoder": (H, 3, 1, False)}[kind]
+    din, dout, nh, ln = dims
+    torch.manual_seed(101)
+    m = MLP(din, H, dout, num_hidden_layers=nh, activation_fn="gelu", use_layer_norm=ln).to(DEV).to(torch.bfloat16)
+    g = torch.Generator(device="cpu").manual_seed(102)
+    x = torch.randn(N, din, generator=g).to(torch.bfloat16).to(DEV).requires_grad_(True)
+    gy = torch.randn(N, dout, generator=g).to(torch.bfloat16).to(DEV)
+    names = ["agn_debug_node32_launches", "agn_debug_enc32_launches", "agn_debug_dec32_launches",
+             "agn_debug_node32_bwd_launches", "agn_debug_dec32_bwd_launches"]
+    c0 = [_counter(n) for n in names]
+    y = m(x)
+    y.backward(gy)
+    torch.cuda.synchronize()
+    assert [_counter(n) for n in names] == c0
+    m64 = MLP(din, H, dout, num_hidden_layers=nh, activation_fn="gelu", use_layer_norm=ln).to(DEV).double()
+    m64.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+    x64 = x.detach().double().requires_grad_(True)
+    import torch.nn.functional as F
+    h = x64
+    for i, lin in enumerate(m64.layers):  # the reference's forward (mlp.py:40-51) in float64
+        h = lin(h)
+        if i < len(m64.layers) - 1:
+            h = F.gelu(h)
+    if ln:
+        h = m64.layer_norm(h)
+    h.backward(gy.double())
+    res = {"y": rel_l2(y.detach().double(), h.detach()), "dx": rel_l2(x.grad.double(), x64.grad)}
+    for (n1, p1), (n2, p2) in zip(m.named_parameters(), m64.named_parameters()):
+        res[n1] = rel_l2(p1.grad.double(), p2.grad)
+    worst = max(res.values())
+    print(f"gelu {kind} N={N}: " + ", ".join(f"{k} {v:.2e}" for k, v in res.items()))
+    # bf16 activations and gradients, no ReLU kinks: ~4e-3 per rounding, a few roundings deep
+    assert worst <= 3e-2, res

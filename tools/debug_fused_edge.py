@@ -54,7 +54,7 @@ def main():
                       ln_partial=part)
     de_f = torch.empty_like(e)
     g0_f = torch.empty(E, H, dtype=dt, device=dev)
-    dW, db, lnp, nblk = core.edge_bwd_fused(rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
+    dW, db, lnp, nblk = core.edge_bwd_fused(rows=E, wpk=es.wpk(), wtpk0=es.wtpk()[0], bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
                                             src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de_f, g0=g0_f)
     torch.cuda.synchronize()
     for name, a, b in (("G0", g0_f, gpre[0]), ("de", de_f, de_s)):

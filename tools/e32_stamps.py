@@ -47,7 +47,7 @@ def main(nu=1000):
     for name, src, dst in (("real ids", lv.src, lv.dst), ("all ids 0", zeros, zeros)):
         def fwd():
             core.edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=src, dst=dst,
-                              out=out, tiles32=True)
+                              out=out)
         for _ in range(3):
             fwd()
         torch.cuda.synchronize()

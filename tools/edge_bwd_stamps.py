@@ -3,6 +3,8 @@ sized layer (1M nodes / ~6M edges), the -DAGN_EB_STAMPS library (AEROGNN_LIB), s
 phase of the chain waves of blocks 0 and 128 (8 tiles each) and the dW waves' wait share.
 
 Usage (GPU): AEROGNN_LIB=aero-gnn_amd/aerognn/libaerognn_stamps.so python tools/edge_bwd_stamps.py
+SAVED=1 (default): the recompute starts from the forward's a1 / statistics; SCR=1 (default): a2 / a3
+through the L2 scratch (the "recompute a2,a3" phase then covers the a3 read-back wait only).
 """
 import os
 import sys
@@ -46,13 +48,21 @@ def main():
     core.proj_forward(N, x, spec.pack["proj"], spec.pack["proj_b"], P)
     de = torch.empty_like(e)
     g0 = torch.empty(E, H, dtype=dt, device=dev)
-    # DPD=1: with dP_d on the dW waves (the product default since round 5)
-    dpd = torch.empty(N, H, dtype=dt, device=dev) if os.environ.get("DPD", "1") == "1" else None
-    print(f"dP_d on the dW waves: {dpd is not None}")
+
+    saved = os.environ.get("SAVED", "1") == "1"
+    scr = os.environ.get("SCR", "1") == "1"
+    a1 = lnst = None
+    if saved:
+        a1 = core.tiled_empty(E, H, dt, e.device)
+        lnst = torch.empty(E, 2, dtype=torch.float32, device=dev)
+        core.edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=lv.src, dst=lv.dst,
+                          out=torch.empty_like(e), a1=a1, stats=lnst)
+    print(f"saved a1 / statistics: {saved}; a2 / a3 scratch: {scr}")
 
     def run():
-        return core.edge_bwd_fused(rows=E, wpk=es.wpk(), bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
-                                   src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de, g0=g0, dpd=dpd, rowptr=lv.rowptr)
+        return core.edge_bwd_fused(rows=E, wpk=es.wpk(), wtpk0=es.wtpk()[0], bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
+                                   src=lv.src, dst=lv.dst, g=ge, g2=dagg, de=de, g0=g0,
+                                   a1=a1, stats=lnst, scratch=scr)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -97,8 +107,7 @@ def main():
         for dwv in range(4):
             s = st[sel, 4 + dwv]
             print(f"  dW wave {dwv}: waited {s[0, 0]} of {s[0, 1]} cycles ({s[0, 0] / max(s[0, 1], 1):.2f}), items {s[0, 2]}"
-                  + (f"; dP_d per L1 pair: G0 recompute {s[0, 3] / max(s[0, 2] / 6, 1):.0f}, walk "
-                     f"{s[0, 4] / max(s[0, 2] / 6, 1):.0f} cycles" if s[0, 3] else ""))
+                  )
 
 
 if __name__ == "__main__":

@@ -48,10 +48,10 @@ def main():
     zeros = torch.zeros_like(lv.dst)
     cases = (("real ids", lv.src, lv.dst), ("src := dst", lv.dst, lv.dst), ("all ids 0", zeros, zeros))
     for ids_name, src, dst in cases[:1] if args.real_only else cases:
-        for kname, t32 in (("edge16 (16-row)", False), ("edge32 (32-row)", True)):
+        for kname in ("edge32 (32-row)",):
             def f():
                 core.edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=src, dst=dst,
-                                  out=out, tiles32=t32)
+                                  out=out)
             for _ in range(2):
                 f()
             torch.cuda.synchronize()
