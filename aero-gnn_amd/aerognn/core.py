@@ -421,7 +421,8 @@ def _poll_faults():
     st = _fault
     if not st["hooked"]:
         import atexit
-        torch.optim.optimizer.register_optimizer_step_pre_hook(_step_pre_hook)
+        from torch.optim.optimizer import register_optimizer_step_pre_hook
+        register_optimizer_step_pre_hook(_step_pre_hook)
         atexit.register(_exit_check)
         st["hooked"] = True
     _fault_read(False)
@@ -543,8 +544,11 @@ class WGrad:
     slice of a wider dW); run() launches ceil(n/8) kernels (+ their fixed-order reductions).
     """
 
-    def __init__(self):
+    def __init__(self, tag="wgrad"):
         self.items = []
+        # kernel-table tag of the launches (bench.py): wgrad_edge (E-row edge chains), wgrad_node
+        # (W_s / W_d and the node MLP), wgrad_enc (encoders, decoder, other MLPs)
+        self.tag = tag
 
     def add(self, G, X, dw, db=None, xidx=None):
         """xidx: X is gathered, row r of the operand = X[xidx[r]] (int32, one entry per row of G)."""
@@ -598,7 +602,7 @@ class WGrad:
             io = sum(logical_rows(G) * (G.shape[1] + X.shape[1]) * s_el + 4 * G.shape[1] * (X.shape[1] + 1)
                      for G, X, _, _, _ in live)
             fl = sum(2.0 * logical_rows(G) * G.shape[1] * X.shape[1] for G, X, _, _, _ in live)
-            with timed("wgrad", (0.0, fl, io)):
+            with timed(self.tag, (0.0, fl, io)):
                 check(lib.agn_wgrad(C.byref(b), dt_code(live[0][0].dtype), 0, stream()), "wgrad")
         self.items = []
 

@@ -136,14 +136,14 @@ def _alloc_gpre(spec, rows, dtype, dev, rowmajor=()):
     return out
 
 
-def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk, wg=None):
+def _chain_param_grads(spec, gpre, inputs0, acts, lnp_partial, nblk, wg=None, tag="wgrad_enc"):
     """Grads (in spec.params() order) from stored pre-activation grads.
 
     Queues the dW/db products on `wg` (a core.WGrad); the returned fp32 tensors are filled
     when wg.run() executes (run here if no batch object is passed in).
     """
     own = wg is None
-    wg = wg or WGrad()
+    wg = wg or WGrad(tag)
     grads = []
     dev = gpre[0].device
     for l, (w, b) in enumerate(spec.linears):
@@ -542,10 +542,10 @@ class GMPFn(torch.autograd.Function):
             # E-row (edge chain) and N-row (projection, node chain) weight gradients go to separate
             # agn_wgrad launches: one split count serves all descs of a launch, and mixing 6x
             # different row counts leaves most workgroups idle behind the edge descs (measured)
-            wg = WGrad()
+            wg = WGrad("wgrad_node")
             if fused:
                 dwe = torch.empty(H, H, dtype=torch.float32, device=dev)
-                we = WGrad()
+                we = WGrad("wgrad_edge")
                 we.add(g0, e, dwe)
                 we.run()
                 eg = [dwe]
@@ -554,7 +554,7 @@ class GMPFn(torch.autograd.Function):
                 eg = eg[:1] + [t if t.dtype == p.dtype else t.to(p.dtype) for t, p in zip(eg[1:], es.params()[1:7])]
                 eg += list(_ln_grads(part_e, nb_e, H, es.ln[0].dtype))
             else:
-                eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e)
+                eg = _chain_param_grads(es, gpre_e, e, ea, part_e, nb_e, tag="wgrad_edge")
             dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dbd = torch.empty(H, dtype=torch.float32, device=dev)
@@ -572,8 +572,8 @@ class GMPFn(torch.autograd.Function):
             segment_sum2(N, H, dx, (lv.rowptr_src, lv.perm_src, dxs), (lv.rowptr, None, dxd), dx)
             xs, xd = (x, lv.src), (x, lv.dst)
             grads_edge = _chain_param_grads(es, gpre_e, [xs, xd, e] if spec.gmp_order else [e, xs, xd],
-                                            ea, part_e, nb_e)
-        grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n)
+                                            ea, part_e, nb_e, tag="wgrad_edge")
+        grads_node = _chain_param_grads(ns, gpre_n, [x, agg], na, part_n, nb_n, tag="wgrad_node")
         return (dx, de, None, None, None, *grads_edge, *grads_node)
 
 
@@ -746,9 +746,9 @@ class EdgeBlockFn(torch.autograd.Function):
             mlp_forward(rows=N, dtype=dt, hidden=H, nlin=1, out_dim=H,
                         segs=[(L.SEG_PLAIN, H, H, dPs, None, None), (L.SEG_PLAIN, H, H, dPd, None, None)],
                         wpk=[spec.pack["projT"]], bias=[None], out=dx)
-            eg = _chain_param_grads(es, gpre, e, ea, part, nb)
+            eg = _chain_param_grads(es, gpre, e, ea, part, nb, tag="wgrad_edge")
             eb = spec.eb
-            wg = WGrad()
+            wg = WGrad("wgrad_node")
             dws = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dwd = torch.empty(H, x.shape[1], dtype=torch.float32, device=dev)
             dbd = torch.empty(H, dtype=torch.float32, device=dev)
@@ -759,7 +759,7 @@ class EdgeBlockFn(torch.autograd.Function):
         else:
             dx = segment_sum2(N, H, None, (lv.rowptr_src, lv.perm_src, dxs), (lv.rowptr, None, dxd),
                               torch.empty(N, H, dtype=dt, device=dev))
-            grads = _chain_param_grads(es, gpre, [e, (x, lv.src), (x, lv.dst)], ea, part, nb)
+            grads = _chain_param_grads(es, gpre, [e, (x, lv.src), (x, lv.dst)], ea, part, nb, tag="wgrad_edge")
         return (dx, de, None, None, None, *grads)
 
 
@@ -804,7 +804,7 @@ class NodeBlockFn(torch.autograd.Function):
                      din=[(H, dx, False), (H, dagg, False)], ln_partial=part)
         de = torch.empty_like(e)
         gather_rows(E, H, lv.dst, dagg, de, cnt_ptr=lv.rowptr if spec.aggregation == "mean" else None)
-        grads = _chain_param_grads(ns, gpre, [x, agg], na, part, nb)
+        grads = _chain_param_grads(ns, gpre, [x, agg], na, part, nb, tag="wgrad_node")
         return (dx, de, None, None, None, *grads)
 
 

@@ -43,17 +43,8 @@ constexpr int NR = 64;                 // acc registers per row half
 constexpr int CW = 4;                  // chain waves
 constexpr int NWAVE = 8;               // chain + dW waves
 constexpr int NTHR = 64 * NWAVE;
-#ifndef AGN_EB_RELOAD_LATE
-#define AGN_EB_RELOAD_LATE 0  // (A/B) the g / g2 re-reads for de issued after the L1 hand-off instead of before it
-#endif
-#ifndef AGN_EB_WE_LDS
-#define AGN_EB_WE_LDS 0  // (A/B) W_e's image in LDS (the round-5 layout, 3 ring slots) instead of L2 fragments
-#endif
-#ifndef AGN_EB_G0_EARLY
-#define AGN_EB_G0_EARLY 0  // (A/B) G0 stored before de's W_e GEMM (round 5 order) instead of after it
-#endif
 #ifndef AGN_EB_NSLOT
-#define AGN_EB_NSLOT (AGN_EB_WE_LDS ? 3 : 7)
+#define AGN_EB_NSLOT 7
 #endif
 constexpr int NSLOT = AGN_EB_NSLOT;    // ring slots (8 KB each; a tile's hand-off pair takes two)
 #ifndef AGN_EB_GROUP
@@ -65,8 +56,7 @@ constexpr int HALF_B = 16 * H * 2;     // 16 rows of one item matrix (4 KB)
 constexpr int SLOT_B = 2 * HALF_B;     // G half + a half
 // LDS images of Lin1..Lin3 at (l - 1) * IMG_B; W_e is read from L2 (packed fragments, 32 KB shared by
 // every CU): its 32 KB of LDS went to the ring, 3 -> 7 slots (round 6)
-constexpr int IMG1 = AGN_EB_WE_LDS ? 1 : 0;  // image index of Lin1 (W_e at 0 when it is in LDS)
-constexpr int OFF_RING = (3 + IMG1) * IMG_B;
+constexpr int OFF_RING = 3 * IMG_B;
 constexpr int OFF_PV = OFF_RING + NSLOT * SLOT_B;  // fp32 [4][H]: b1, b2, b3, LN gamma
 constexpr int OFF_FLAG = OFF_PV + 4 * H * 4;       // int filled[NSLOT], consumed[NSLOT]
 constexpr int OFF_LNP = OFF_FLAG + 8 * ((2 * NSLOT + 7) / 8) * 4;  // fp32 [CW][2][H]: LayerNorm partials per chain wave
@@ -302,12 +292,19 @@ typedef short s16x8v __attribute__((ext_vector_type(8)));
 AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const BOp<bf16, NR>& act) {
 #pragma unroll
   for (int i = 0; i < NR / 8; ++i) {
-    const u32x4 m = __builtin_bit_cast(u32x4, (s16x8v{} - __builtin_bit_cast(s16x8v, act.u[i])) >> 15);
+    // relu outputs are +0 or positive int16 patterns: min(a, 1) as unsigned 16-bit is 1 exactly when
+    // a > 0, and the rounded dA times that 0 / 1 is the masked value bit for bit (3 VALU per dword
+    // instead of v_pk_sub + v_pk_ashr + v_and + v_cvt_pk). Inline asm: written with 16-bit vector
+    // builtins, this hipcc applied dword 0's mask to all four dwords of the unit (the miscompile above)
+    const u32x4 a4 = __builtin_bit_cast(u32x4, act.u[i]);
     u32x4 w;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = 8 * i + 2 * k;
-      w[k] = pack2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]) & m[k];
+      const uint32_t g = pack2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]);
+      uint32_t m;
+      asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(m) : "v"(a4[k]));  // (the constant 1 for both halves)
+      asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(w[k]) : "v"(g), "v"(m));
     }
     out.u[i] = __builtin_bit_cast(bf16x8, w);
   }
@@ -370,7 +367,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   // wave instruction)
   uint4* const scr = SCR ? reinterpret_cast<uint4*>(a.scratch) + (size_t)(blockIdx.x * CW + cw) * 1024 : nullptr;
   if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
-
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
     if (cw >= cmax) continue;
@@ -434,8 +430,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         BOp<bf16, NR> eop;
         eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
         EB_STAMP(1);
-        if (AGN_EB_WE_LDS) gemm_rows(acc, eop, lds, fresh_lane(lane));
-        else gemm_rows_g(acc, eop, reinterpret_cast<const uint4*>(a.wpk[0]), fresh_lane(lane));
+        gemm_rows_g(acc, eop, reinterpret_cast<const uint4*>(a.wpk[0]), fresh_lane(lane));
       }
       cbarrier();
       a1.template set_relu<NT>(acc);
@@ -445,7 +440,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     pin(a1);
     sched_fence();
     acc_bias(acc, pv + 0 * H, h);
-    gemm_rows(acc, a1, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
+    gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
     cbarrier();
     {  // a2 is not kept (recomputed from a1 in step 2, or parked in the scratch)
       BOp<bf16, NR> a2;
@@ -458,7 +453,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       }
       sched_fence();
       acc_bias(acc, pv + 1 * H, h);
-      gemm_rows(acc, a2, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a2, lds + 1 * IMG_B, fresh_lane(lane));
     }
     cbarrier();
     {  // a3 is not kept either (recomputed in step 3, or parked in the scratch)
@@ -472,7 +467,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       }
       sched_fence();
       acc_bias(acc, pv + 2 * H, h);
-      gemm_rows(acc, a3, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a3, lds + 2 * IMG_B, fresh_lane(lane));
     }
     EB_STAMP(2);
     // LayerNorm statistics (mlp_fwd_res_kernel's epilogue)
@@ -616,7 +611,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int i = 0; i < NR / 8; ++i) a2.u[i] = __builtin_bit_cast(bf16x8, scr[64 * i + l]);
       }
       EB_STAMP(5);
-      gemm_cols(acc, op, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
+      gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
       cbarrier();
       relu_select_pk(op, acc, a3s);  // G2
       EB_STAMP(6);
@@ -625,13 +620,13 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       BOp<bf16, NR> a3;
       sched_fence();
       acc_bias(acc, pv + 0 * H, h);
-      gemm_rows(acc, a1, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
       cbarrier();
       a2.template set_relu<NT>(acc);
       pin(a2);
       sched_fence();
       acc_bias(acc, pv + 1 * H, h);
-      gemm_rows(acc, a2, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
+      gemm_rows(acc, a2, lds + 1 * IMG_B, fresh_lane(lane));
       cbarrier();
       a3.template set_relu<NT>(acc);
       pin(a3);
@@ -639,7 +634,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       EB_STAMP(4);
       produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
       EB_STAMP(5);
-      gemm_cols(acc, op, lds + (IMG1 + 2) * IMG_B, fresh_lane(lane));
+      gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
       cbarrier();
       relu_select_pk(op, acc, a3);  // G2
       EB_STAMP(6);
@@ -647,7 +642,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
-    gemm_cols(acc, op, lds + (IMG1 + 1) * IMG_B, fresh_lane(lane));
+    gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a2);  // G1
     EB_STAMP(8);
@@ -668,11 +663,10 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
       }
     };
-    if (!AGN_EB_RELOAD_LATE) reload_g();
+    reload_g();
     produce_pair(lds, nbase + 4 * gsz, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
-    if (AGN_EB_RELOAD_LATE) reload_g();
-    gemm_cols(acc, op, lds + (IMG1 + 0) * IMG_B, fresh_lane(lane));
+    gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a1);  // G0
     EB_STAMP(10);
@@ -680,11 +674,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
     // de = G0 W_e first, G0's stores after it: vmcnt retires loads and stores in issue order, so W_e's
     // fragment loads issued behind the G0 stores would each wait for those stores too
-    if (AGN_EB_G0_EARLY) op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
-    if (AGN_EB_WE_LDS) gemm_cols(acc, op, lds, fresh_lane(lane));
-    else gemm_cols_g(acc, op, reinterpret_cast<const uint4*>(a.wtpk0), fresh_lane(lane));
+    gemm_cols_g(acc, op, reinterpret_cast<const uint4*>(a.wtpk0), fresh_lane(lane));
     sched_fence();
-    if (!AGN_EB_G0_EARLY) op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
+    op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
     {
       float v[NR];
 #pragma unroll
@@ -846,12 +838,12 @@ __global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_
   __shared__ __attribute__((aligned(16))) char lds[LDS_B];
   // weight images from the packed forward operands: unit (ot, ku, lane) -> row 32ot + lane%32,
   // chunk 2ku + lane/32
-  for (int l = 1 - IMG1; l < 4; ++l) {
+  for (int l = 1; l < 4; ++l) {
     const uint4* src = reinterpret_cast<const uint4*>(a.wpk[l]);
     for (int u = threadIdx.x; u < 2048; u += NTHR) {
       const int ln = u & 63, unit = u >> 6;
       const int o = 32 * (unit >> 3) + (ln & 31), ch = 2 * (unit & 7) + (ln >> 5);
-      *reinterpret_cast<uint4*>(lds + (l - 1 + IMG1) * IMG_B + aoff(o, ch)) = src[u];
+      *reinterpret_cast<uint4*>(lds + (l - 1) * IMG_B + aoff(o, ch)) = src[u];
     }
   }
   float* pv = reinterpret_cast<float*>(lds + OFF_PV);

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--nu", type=int, default=1000)
+    ap.add_argument("--only", default=None, help="substring filter on the case names")
     args = ap.parse_args()
     from aerognn import core
     from aerognn.graph import Level
@@ -67,6 +68,8 @@ def main():
         for scr in (True, False):
             cases[f"bwd saved={int(saved)} scratch={int(scr)}"] = bwd(saved, scr)
     cases["segment_sum (dP_d)"] = lambda: core.segment_sum(N, H, lv.rowptr, None, g0, dpd)
+    if args.only:
+        cases = {k: v for k, v in cases.items() if args.only in k}
     fwd(True)()
     for f in cases.values():
         f()

@@ -19,9 +19,11 @@ import sys
 
 # bench.py tag -> kernel names of the launch it times (bf16 H=128 C3 workload), first present wins:
 # `edge_bwd` is the fused edge backward by default, the split path's resident backward otherwise
-TAGS = {"edge_bwd": ("edge_bwd_fused_kernel", "mlp_bwd_res_kernel"), "edge_fwd": ("mlp_fwd_res_kernel",),
-        "wgrad": ("wgrad_kernel",), "segment_sum": ("segment_sum_kernel",), "gather_rows": ("gather_rows_kernel",),
-        "node_fwd": ("mlp_fwd_kernelIDF16bLi4ELi0E",), "node_bwd": ("mlp_bwd_kernelIDF16bLi4ELi0E",)}
+TAGS = {"edge_bwd": ("edge_bwd_fused_kernel", "mlp_bwd_res_kernel"), "edge_fwd": ("edge32_fwd_kernel", "mlp_fwd_res_kernel"),
+        "wgrad": ("wgrad_kernel",), "segment_sum": ("segment_sum4_kernel", "segment_sum_kernel"),
+        "gather_rows": ("gather_rows4_kernel", "gather_rows_kernel"),
+        "node_fwd": ("node32_fwd_kernel", "mlp_fwd_kernelIDF16bLi4ELi0E"),
+        "node_bwd": ("node32_bwd_kernel", "mlp_bwd_kernelIDF16bLi4ELi0E")}
 
 
 def _rows(d):
