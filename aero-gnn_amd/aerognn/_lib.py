@@ -83,7 +83,8 @@ class EdgeBwdArgs(C.Structure):
     _fields_ = [("rows", i32), ("nblk", i32), ("wpk", vp * 4), ("bias", vp * 4), ("ln_g", vp), ("e", vp),
                 ("proj", vp), ("src", vp), ("dst", vp), ("g", vp), ("g2", vp), ("de", vp), ("g0", vp),
                 ("dw_partial", vp), ("db_partial", vp), ("ln_partial", vp), ("stamps", vp),
-                ("a1", vp), ("stats", vp), ("scratch", vp), ("wtpk0", vp)]
+                ("a1", vp), ("stats", vp), ("scratch", vp), ("wtpk0", vp),
+                ("xk", i32), ("xld", i32)]
 
 
 class EdgeFwdArgs(C.Structure):
@@ -128,7 +129,7 @@ LAUNCHES = ("agn_pack", "agn_mlp_forward", "agn_mlp_backward", "agn_reduce_parti
             "agn_pool_edge_sort", "agn_pool_edge_emit", "agn_bfs_distance", "agn_center_seed", "agn_maxdeg_seed",
             "agn_bistride_select", "agn_index_map", "agn_subgraph_edges", "agn_scatter_rows", "agn_wec_forward",
             "agn_wec_backward", "agn_edge_features", "agn_node_features", "agn_normalize", "agn_col_stats", "agn_collate",
-            "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_wgrad_reduce",
+            "agn_segment_max", "agn_segment_max_backward", "agn_edge_bwd_fused", "agn_encoder_bwd_fused", "agn_wgrad_reduce",
             "agn_edge_forward32",
             "agn_proj_forward", "agn_proj_backward")
 
@@ -228,6 +229,7 @@ def lib():
             "agn_col_stats": (i32, [i32, i32, vp, i32, vp, vp, C.c_float, vp, vp]),
             "agn_collate": (i32, [i32, C.c_int64, C.c_int64, vp, vp, vp, vp, vp]),
             "agn_edge_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
+            "agn_encoder_bwd_fused": (i32, [C.POINTER(EdgeBwdArgs), vp]),
             "agn_edge_fwd32_blocks": (i32, [i32]),
             "agn_edge_forward32": (i32, [C.POINTER(EdgeFwdArgs), vp]),
             "agn_debug_node32_launches": (C.c_long, []),

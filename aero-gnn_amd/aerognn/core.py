@@ -471,6 +471,12 @@ def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de
             raise L.AeroGNNError(f"agn_edge_bwd_fused: device fault word {f:#x} (LDS ring wait timed out; dW invalid)")
     else:
         _poll_faults()
+    return _reduce_slabs(rows, dwp, dbp, lnp, nblk, dev)
+
+
+def _reduce_slabs(rows, dwp, dbp, lnp, nblk, dev):
+    """dW1..dW3 / db1..db3 from a fused backward's per-block slabs (fixed order, agn_wgrad_reduce)."""
+    H = 128
     dw = torch.empty(3, H, H, dtype=torch.float32, device=dev)
     db = torch.empty(3, H, dtype=torch.float32, device=dev)
     b = L.WgradBatch()
@@ -478,8 +484,52 @@ def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de
     for l in range(3):
         b.d[l] = L.WgradDesc(None, None, H, H, H, H, int(rows), H, ptr(dwp[l * nblk * H * H:]), ptr(dbp[l * nblk * H:]),
                              ptr(dw[l]), ptr(db[l]), 0, 0, nblk, 0)
-    check(lib.agn_wgrad_reduce(C.byref(b), nblk, stream()), "wgrad_reduce")
+    check(L.lib().agn_wgrad_reduce(C.byref(b), nblk, stream()), "wgrad_reduce")
     return dw, db, lnp, nblk
+
+
+def encoder_fused_ok(spec, dtype, k, rows, need_dx):
+    """agn_encoder_bwd_fused applies (training): a bf16 encoder MLP of 4 Linears (k <= 16 inputs, H = 128
+    hidden and out, ReLU, LayerNorm) on >= 65,536 rows whose input needs no gradient (the model's
+    node / edge features). Then the forward saves nothing and the backward recomputes the chain on
+    chip with dW1..dW3 there. AEROGNN_FUSED_ENC_BWD=0 selects the split path."""
+    import os
+    return (os.environ.get("AEROGNN_FUSED_ENC_BWD", "1") != "0" and dtype == torch.bfloat16 and not need_dx
+            and spec.hidden == 128 and spec.out_dim == 128 and spec.nlin == 4 and spec.ln is not None
+            and spec.act == L.ACT["relu"] and 1 <= k <= 16 and rows >= 64 * 1024)
+
+
+def encoder_bwd_fused(*, rows, wpk, bias, ln_g, x, xidx, g, g0, tag=None, cost=None):
+    """agn_encoder_bwd_fused: (dW1..dW3, db1..db3, LayerNorm partials, nblk) of an encoder chain, and
+    G0 into g0 ([rows, 128] row-major) for dW0 / db0; x [n, k] bf16 (rows gathered by xidx, int32,
+    when given)."""
+    lib = L.lib()
+    dev = g.device
+    H = 128
+    nblk = int(lib.agn_edge_bwd_blocks(int(rows)))
+    dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
+    dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
+    lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
+    scr = torch.empty(int(lib.agn_edge_bwd_scratch_bytes(nblk)), dtype=torch.uint8, device=dev)
+    a = L.EdgeBwdArgs()
+    a.rows, a.nblk = int(rows), nblk
+    for i in range(4):
+        a.wpk[i] = wpk[i]
+        a.bias[i] = bias[i]
+    a.ln_g = ln_g
+    a.e, a.src, a.g, a.g0 = ptr(x), ptr(xidx), ptr(g), ptr(g0)
+    a.dw_partial, a.db_partial, a.ln_partial, a.scratch = ptr(dwp), ptr(dbp), ptr(lnp), ptr(scr)
+    a.xk, a.xld = int(x.shape[1]), int(x.stride(0))
+    a.stamps = ptr(STAMPS)
+    with timed(tag, cost):
+        check(lib.agn_encoder_bwd_fused(C.byref(a), stream()), "encoder_bwd_fused")
+    if CHECK_FAULTS:
+        f = L.fault_status(reset=True)
+        if f:
+            raise L.AeroGNNError(f"agn_encoder_bwd_fused: device fault word {f:#x} (LDS ring wait timed out; dW invalid)")
+    else:
+        _poll_faults()
+    return _reduce_slabs(rows, dwp, dbp, lnp, nblk, dev)
 
 
 def reduce_partials(partial, nw, n, out):

@@ -196,7 +196,9 @@ class MLPFn(torch.autograd.Function):
         nrow = x.shape[0] if rows is None else rows.numel()
         dt = x.dtype
         out = torch.empty(nrow, spec.out_dim, dtype=dt, device=x.device)
-        acts, hpre, stats = _alloc_saves(spec, nrow, dt, x.device, train)
+        # an encoder whose input needs no gradient trains on the fused backward (the forward saves nothing)
+        fused = train and _core.encoder_fused_ok(spec, dt, x.shape[1], nrow, ctx.needs_input_grad[0])
+        acts, hpre, stats = _alloc_saves(spec, nrow, dt, x.device, train and not fused)
         ks = _ksegs(x, spec.hidden)
         if len(ks) > L.MAX_SEG:
             raise NotImplementedError("aerognn MLP input wider than 3 x hidden")
@@ -209,7 +211,7 @@ class MLPFn(torch.autograd.Function):
         mlp_forward(rows=nrow, dtype=dt, hidden=spec.hidden, nlin=spec.nlin, act_fn=spec.act, out_dim=spec.out_dim,
                     segs=segs, wpk=spec.wpk(), bias=spec.biases(), ln=spec.lnp(), out=out,
                     acts=acts, hpre=hpre, stats=stats)
-        ctx.spec, ctx.idx, ctx.nrow = spec, idx, nrow
+        ctx.spec, ctx.idx, ctx.nrow, ctx.fused = spec, idx, nrow, fused
         ctx.acts, ctx.hpre, ctx.stats = acts, hpre, stats
         ctx.save_for_backward(x)
         return out
@@ -221,6 +223,31 @@ class MLPFn(torch.autograd.Function):
         gy = _c(gy)
         rows = ctx.nrow
         dt = x.dtype
+        if ctx.fused:
+            # one launch: forward recompute, LayerNorm backward, chain rule, dW1..dW3 / db1..db3 on chip;
+            # dW0 / db0 from G0 and the (gathered) input rows on agn_wgrad
+            H = spec.hidden
+            g0 = torch.empty(rows, H, dtype=dt, device=x.device)
+            s_el = x.element_size()
+            dW13, db13, part, nblk = _core.encoder_bwd_fused(
+                rows=rows, wpk=spec.wpk(), bias=spec.biases(), ln_g=spec.lnp()[0], x=x, xidx=ctx.idx, g=gy, g0=g0,
+                tag="enc_bwd", cost=(0.0, 2.0 * rows * H * H * 9, rows * (3 * H * s_el + 2 * x.shape[1] + 4)))
+            w0, b0 = spec.linears[0]
+            dw0 = torch.empty(w0.shape, dtype=torch.float32, device=x.device)
+            db0 = torch.empty(H, dtype=torch.float32, device=x.device) if b0 is not None else None
+            wg = WGrad("wgrad_enc")
+            wg.add(g0, x, dw0, db0, xidx=ctx.idx)
+            wg.run()
+            grads = [dw0] + ([db0] if b0 is not None else [])
+            for l in range(3):
+                w, b = spec.linears[l + 1]
+                grads.append(dW13[l])
+                if b is not None:
+                    grads.append(db13[l])
+            grads += list(_ln_grads(part, nblk, H, torch.float32))
+            params = spec.params()
+            grads = [gr if gr.dtype == p.dtype else gr.to(p.dtype) for gr, p in zip(grads, params)]
+            return (None, None, None, None, *grads)
         gpre = _alloc_gpre(spec, rows, dt, x.device)
         ks = _ksegs(x, spec.hidden)
         need_dx = ctx.needs_input_grad[0]

@@ -336,7 +336,11 @@ AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const B
 // 16-KB slice of a.scratch (L2-resident: the same addresses are rewritten every tile) and are read
 // back for their hand-offs, instead of being recomputed from a1 a second time (64 MFMAs plus their
 // bias / ReLU work per tile).
-template <bool SAVED, bool SCR>
+// ENC: the same chain as an encoder MLP (models/mlp.py:40-51 on the node / edge features,
+// models/bsms_mgn.py:138-139): h0 = x W0^T + b0 on k <= 16 input features (a.e, rows gathered by
+// a.src when set), S = g (no receiver term), and no input gradient: the tile ends with G0's store
+// (dW0 = G0^T x and db0 go to agn_wgrad). Bitwise the split path's (mlp_bwd_res_kernel) G's.
+template <bool SAVED, bool SCR, bool ENC = false>
 AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0) {
 #ifdef AGN_EB_STAMPS
   unsigned long long* stp = nullptr;
@@ -360,6 +364,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
   auto tile_id = [&](int rd) {
     const int row = (rd * CW + cw) * 32 + (lane0 & 31);
     const int rr = row < a.rows ? row : a.rows - 1;
+    if constexpr (ENC) return srcp ? srcp[rr] : rr;  // the input row (gathered or not)
     const int32_t* p = (lane0 < 32 && !SAVED) ? srcp : dstp;  // (SAVED reads no src)
     return p[rr];
   };
@@ -387,7 +392,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int row = tile * 32 + c;
     const bool valid = row < a.rows;
     const int rr = valid ? row : a.rows - 1;
-    const int sid = SAVED ? 0 : ids[c], did = ids[32 + c];
+    const int sid = SAVED ? 0 : ids[c], did = ENC ? 0 : ids[32 + c];
     const bool more = rd + rw.step < rw.end;
     const int nid = tile_id(more ? rd + rw.step : rd);  // stored to the slot before the tile's stores
     // incoming gradient rows g and dAgg[dst]: loaded now, kept raw (64 registers) through the
@@ -402,7 +407,10 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       st = *reinterpret_cast<const f32x2*>(a.stats + 2 * (size_t)rr);
     }
     uint4 graw[NR / 8], g2raw[NR / 8];
-    {
+    if constexpr (ENC) {
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) g2raw[i] = uint4{0u, 0u, 0u, 0u};
+    } else {
       const bf16* g2p = reinterpret_cast<const bf16*>(a.g2) + (size_t)did * H;
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) g2raw[i] = *reinterpret_cast<const uint4*>(g2p + 16 * i + 8 * h);
@@ -417,7 +425,35 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     }
     // ---- forward recompute (mlp_fwd_res_kernel's operations, in its order)
     f32x16 acc[NT];
-    if constexpr (!SAVED) {
+    if constexpr (ENC) {
+      // h0 = x W0^T + b0 (enc32_fwd_kernel's layer 0: the row's k <= 16 features in registers
+      // 4q..4q+3 = features 8q + 4h .. +3 of one k-step, one MFMA per output tile onto the bias)
+      bf16x8 xu;
+      {
+        const bf16* rowp = reinterpret_cast<const bf16*>(a.e) + (size_t)sid * a.xld;
+        float v[8];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x4 x = load4_masked(rowp, 8 * q + 4 * h, a.xk, false);
+          v[4 * q] = x[0]; v[4 * q + 1] = x[1]; v[4 * q + 2] = x[2]; v[4 * q + 3] = x[3];
+        }
+        xu = __builtin_bit_cast(bf16x8, u32x4{pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]), pack2(v[6], v[7])});
+      }
+      EB_STAMP(1);
+      const float* b0 = a.bias[0];
+#pragma unroll
+      for (int q = 0; q < 4 * NT; ++q) {
+        const f32x4 x = b0 ? *reinterpret_cast<const f32x4*>(b0 + 8 * q + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
+      }
+      const uint4* w0 = reinterpret_cast<const uint4*>(a.wpk[0]);
+#pragma unroll
+      for (int ot = 0; ot < NT; ++ot)
+        acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w0[ot * 64 + lane]), xu, acc[ot], 0, 0, 0);
+      cbarrier();
+      a1.template set_relu<NT>(acc);
+    } else if constexpr (!SAVED) {
       {
         {  // acc = P_s[src] + P_d[dst] on the matrix cores (the forward kernel's exact add)
           BOp<bf16, NR> xs, xd;
@@ -499,7 +535,15 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     // ---- incoming gradient S = g + dAgg[dst] (mlp_bwd_res_kernel's load_grad_w)
     float A[NR];
-    {  // S = g + g2 on the matrix cores (exact fp32 add): acc is free once h3 is packed
+    if constexpr (ENC) {  // S = g (mlp_bwd_res_kernel's load_grad_w without a second term)
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+        float x[8];
+        unpack8_w(x, graw[i]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) A[8 * i + e] = x[e];
+      }
+    } else {  // S = g + g2 on the matrix cores (exact fp32 add): acc is free once h3 is packed
       BOp<bf16, NR> og, og2;
       og.set_w(graw);
       og2.set_w(g2raw);
@@ -663,7 +707,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int i = 0; i < NR / 8; ++i) graw[i] = *reinterpret_cast<const uint4*>(gp + 16 * i + 8 * h);
       }
     };
-    reload_g();
+    if constexpr (!ENC) reload_g();
     produce_pair(lds, nbase + 4 * gsz, op, a1, fresh_lane(lane), EB_IST(4));
     EB_STAMP(9);
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
@@ -672,6 +716,14 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
+    if constexpr (ENC) {  // no input gradient: G0 for agn_wgrad's dW0 / db0 ends the tile
+      op.store(reinterpret_cast<bf16*>(a.g0) + (size_t)row * H, h, valid);
+      EB_STAMP(11);
+#ifdef AGN_EB_STAMPS
+      ++ntile_done;
+#endif
+      continue;
+    }
     // de = G0 W_e first, G0's stores after it: vmcnt retires loads and stores in issue order, so W_e's
     // fragment loads issued behind the G0 stores would each wait for those stores too
     gemm_cols_g(acc, op, reinterpret_cast<const uint4*>(a.wtpk0), fresh_lane(lane));
@@ -833,7 +885,7 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
   }
 }
 
-template <bool SAVED, bool SCR>
+template <bool SAVED, bool SCR, bool ENC = false>
 __global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_bwd_args a) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_B];
   // weight images from the packed forward operands: unit (ot, ku, lane) -> row 32ot + lane%32,
@@ -856,7 +908,7 @@ __global__ __launch_bounds__(NTHR, 2) void edge_bwd_fused_kernel(const agn_edge_
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wave < CW) chain_wave<SAVED, SCR>(a, lds, wave, lane);
+  if (wave < CW) chain_wave<SAVED, SCR, ENC>(a, lds, wave, lane);
   else dw_wave(a, lds, wave - CW, lane);
   __syncthreads();
   // LayerNorm parameter partials of the four chain waves, summed in wave order
@@ -936,6 +988,19 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
   else if (saved) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, false>), grid, blk, 0, (hipStream_t)stream, *a);
   else if (scr) hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true>), grid, blk, 0, (hipStream_t)stream, *a);
   else hipLaunchKernelGGL((edge_bwd_fused_kernel<false, false>), grid, blk, 0, (hipStream_t)stream, *a);
+  return launch_status();
+}
+
+int agn_encoder_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
+  if (!a || a->rows < 1 || a->nblk < 1 || !a->e || !a->g || !a->ln_g || !a->g0 || !a->dw_partial || !a->db_partial ||
+      !a->ln_partial || !a->scratch || a->xk < 1 || a->xk > 16 || a->xld < a->xk)
+    return AGN_E_ARG;
+  if ((reinterpret_cast<uintptr_t>(a->scratch) & 15) || (reinterpret_cast<uintptr_t>(a->g) & 15) ||
+      (reinterpret_cast<uintptr_t>(a->g0) & 15))
+    return AGN_E_ARG;
+  for (int l = 0; l < 4; ++l)
+    if (!a->wpk[l] || (reinterpret_cast<uintptr_t>(a->wpk[l]) & 15)) return AGN_E_ARG;
+  hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true, true>), dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

@@ -397,10 +397,21 @@ typedef struct {
   /* packed A = W_e^T (agn_pack trans = 1, bf16): de = G0 W_e + S reads it from L2 (round 6: W_e's
    * LDS image went to the hand-off ring) */
   const void* wtpk0;
+  /* agn_encoder_bwd_fused only: the input's feature count (<= 16) and row stride (elements) */
+  int xk;
+  int xld;
 } agn_edge_bwd_args;
 int agn_edge_bwd_blocks(int rows);
 size_t agn_edge_bwd_scratch_bytes(int nblk);
 int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
+/* The same fused backward for an encoder MLP (mlp.py:40-51 with 4 Linears, ReLU and LayerNorm on
+ * k <= 16 input features: the node / edge encoders of bsms_mgn.py:138-139), when the input needs no
+ * gradient: h0 = x W0^T + b0 is recomputed from the narrow input rows (e = x [rows or gathered
+ * rows][xld], src = the gather index or NULL), S = g (g2 / dst / de / proj / wtpk0 unused), dW1..dW3,
+ * db1..db3 and the LayerNorm partials as agn_edge_bwd_fused; G0 is written for dW0 = G0^T x and db0
+ * (agn_wgrad). The forward then saves nothing (agn_mlp_forward without act / hpre / stats).
+ * scratch is required (agn_edge_bwd_scratch_bytes(nblk)); grid agn_edge_bwd_blocks(rows). */
+int agn_encoder_bwd_fused(const agn_edge_bwd_args* a, void* stream);
 /* Device fault word of the persistent hand-off kernels (agn_edge_bwd_fused's LDS ring): the OR of
  * AGN_FAULT_* bits recorded since the last reset (0 = none). A set bit means a bounded wait gave
  * up and that launch's dW / db are wrong. Synchronises the device; reset != 0 clears the word. */

@@ -293,3 +293,47 @@ def test_gelu_chain_at_resident_sizes(kind):
     print(f"gelu {kind} N={N}: " + ", ".join(f"{k} {v:.2e}" for k, v in res.items()))
     # bf16 activations and gradients, no ReLU kinks: ~4e-3 per rounding, a few roundings deep
     assert worst <= 3e-2, res
+
+
+@pytest.mark.parametrize("rows,k,gather", [(598400, 4, True), (70001, 6, False)])
+def test_encoder_fused_backward_matches_split(rows, k, gather):
+    """Round 6: an encoder whose input needs no gradient trains on agn_encoder_bwd_fused (the forward
+    saves nothing; h0..h3 recomputed, dW1..dW3 on chip, dW0 from G0 on agn_wgrad). Its recompute is
+    bitwise the forward, so its G's equal the split path's (pinned above by the mask-matched float64
+    test) and every parameter gradient matches the split path (AEROGNN_FUSED_ENC_BWD=0) to fp32
+    summation order (models/mlp.py:40-51; the edge encoder reads through the level permutation)."""
+    from models.mlp import MLP
+    from aerognn import core
+    torch.manual_seed(111)
+    m = MLP(k, H, H, num_hidden_layers=2).to(DEV)
+    g = torch.Generator(device="cpu").manual_seed(112)
+    n_in = rows + 55 if gather else rows
+    x = torch.randn(n_in, k, generator=g).to(torch.bfloat16).to(DEV)
+    idx = torch.randperm(n_in, generator=g)[:rows].to(DEV) if gather else None
+    gy = torch.randn(rows, H, generator=g).to(torch.bfloat16).to(DEV)
+
+    def run(fused):
+        os.environ["AEROGNN_FUSED_ENC_BWD"] = "1" if fused else "0"
+        try:
+            m.zero_grad(set_to_none=True)
+            core.PROF = []
+            y = m.forward_rows(x, idx) if gather else m(x)
+            y.backward(gy)
+            torch.cuda.synchronize()
+            tags = [t for t, *_ in core.PROF]
+        finally:
+            core.PROF = None
+            os.environ.pop("AEROGNN_FUSED_ENC_BWD", None)
+        return y.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}, tags
+
+    y1, g1, t1 = run(True)
+    y0, g0, t0 = run(False)
+    assert "enc_bwd" in t1 and "enc_bwd" not in t0
+    assert torch.equal(y1, y0)  # the no-save forward is bitwise the saving one
+    worst = 0.0
+    for n in g0:
+        r = rel_l2(g1[n].double(), g0[n].double())
+        worst = max(worst, r)
+        print(f"encoder fused vs split rows={rows} {n}: rel-L2 {r:.2e}")
+        assert r <= 1e-5, (n, r)
+    print(f"encoder fused vs split rows={rows}: worst {worst:.2e}")
