@@ -437,8 +437,9 @@ def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de
     """agn_edge_bwd_fused; returns (dW1..dW3 [3,128,128] fp32, db1..db3 [3,128] fp32, LayerNorm
     partials [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce).
     a1 / stats: the forward's saves (agn_edge_forward32);
-    then e, proj and src are not read. scratch None: AEROGNN_EB_SCRATCH (default on) decides whether
-    a2 / a3 go through the L2 scratch instead of a second recompute (bitwise the same outputs)."""
+    then e, proj and src are not read. scratch None: AEROGNN_EB_SCRATCH (default off) decides whether
+    a2 / a3 go through a scratch buffer instead of a second recompute (bitwise the same outputs; not
+    faster, and its slices leave L2: DESIGN.md §9 round 6)."""
     import os
     lib = L.lib()
     dev = g2.device
@@ -448,7 +449,7 @@ def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de
     dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
     lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
     if scratch is None:
-        scratch = os.environ.get("AEROGNN_EB_SCRATCH", "1") != "0"
+        scratch = os.environ.get("AEROGNN_EB_SCRATCH", "0") == "1"
     scr = (torch.empty(int(lib.agn_edge_bwd_scratch_bytes(nblk)), dtype=torch.uint8, device=dev)
            if scratch else None)
     a = L.EdgeBwdArgs()
@@ -510,7 +511,9 @@ def encoder_bwd_fused(*, rows, wpk, bias, ln_g, x, xidx, g, g0, tag=None, cost=N
     dwp = torch.empty(3 * nblk * H * H, dtype=torch.float32, device=dev)
     dbp = torch.empty(3 * nblk * H, dtype=torch.float32, device=dev)
     lnp = torch.empty(nblk, 2 * H, dtype=torch.float32, device=dev)
-    scr = torch.empty(int(lib.agn_edge_bwd_scratch_bytes(nblk)), dtype=torch.uint8, device=dev)
+    import os
+    scr = (torch.empty(int(lib.agn_edge_bwd_scratch_bytes(nblk)), dtype=torch.uint8, device=dev)
+           if os.environ.get("AEROGNN_EB_SCRATCH", "0") == "1" else None)
     a = L.EdgeBwdArgs()
     a.rows, a.nblk = int(rows), nblk
     for i in range(4):

@@ -993,14 +993,15 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
 
 int agn_encoder_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
   if (!a || a->rows < 1 || a->nblk < 1 || !a->e || !a->g || !a->ln_g || !a->g0 || !a->dw_partial || !a->db_partial ||
-      !a->ln_partial || !a->scratch || a->xk < 1 || a->xk > 16 || a->xld < a->xk)
+      !a->ln_partial || a->xk < 1 || a->xk > 16 || a->xld < a->xk)
     return AGN_E_ARG;
   if ((reinterpret_cast<uintptr_t>(a->scratch) & 15) || (reinterpret_cast<uintptr_t>(a->g) & 15) ||
       (reinterpret_cast<uintptr_t>(a->g0) & 15))
     return AGN_E_ARG;
   for (int l = 0; l < 4; ++l)
     if (!a->wpk[l] || (reinterpret_cast<uintptr_t>(a->wpk[l]) & 15)) return AGN_E_ARG;
-  hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true, true>), dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
+  if (a->scratch) hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true, true>), dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
+  else hipLaunchKernelGGL((edge_bwd_fused_kernel<false, false, true>), dim3(a->nblk), dim3(NTHR), 0, (hipStream_t)stream, *a);
   return launch_status();
 }
 

@@ -391,8 +391,9 @@ typedef struct {
   const void* a1;
   const float* stats;
   /* optional: [nblk][4][2][32][128] bf16 (64 KB per block, agn_edge_bwd_scratch_bytes), the chain
-   * waves' a2 / a3 parked between the recompute and their hand-offs (L2-resident: rewritten every
-   * tile). NULL = a2 / a3 recomputed a second time from a1. Outputs are bitwise the same. */
+   * waves' a2 / a3 parked between the recompute and their hand-offs instead of recomputed a second
+   * time from a1. Outputs are bitwise the same. Not the default: the slices do not stay in L2 (PMC:
+   * +3 GB written per C3 level-0 launch) and the launch is no faster. */
   void* scratch;
   /* packed A = W_e^T (agn_pack trans = 1, bf16): de = G0 W_e + S reads it from L2 (round 6: W_e's
    * LDS image went to the hand-off ring) */
@@ -410,7 +411,7 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream);
  * rows][xld], src = the gather index or NULL), S = g (g2 / dst / de / proj / wtpk0 unused), dW1..dW3,
  * db1..db3 and the LayerNorm partials as agn_edge_bwd_fused; G0 is written for dW0 = G0^T x and db0
  * (agn_wgrad). The forward then saves nothing (agn_mlp_forward without act / hpre / stats).
- * scratch is required (agn_edge_bwd_scratch_bytes(nblk)); grid agn_edge_bwd_blocks(rows). */
+ * scratch as for agn_edge_bwd_fused (optional); grid agn_edge_bwd_blocks(rows). */
 int agn_encoder_bwd_fused(const agn_edge_bwd_args* a, void* stream);
 /* Device fault word of the persistent hand-off kernels (agn_edge_bwd_fused's LDS ring): the OR of
  * AGN_FAULT_* bits recorded since the last reset (0 = none). A set bit means a bounded wait gave

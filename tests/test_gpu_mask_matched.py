@@ -295,8 +295,9 @@ def test_gelu_chain_at_resident_sizes(kind):
     assert worst <= 3e-2, res
 
 
+@pytest.mark.parametrize("scratch", ["0", "1"])
 @pytest.mark.parametrize("rows,k,gather", [(598400, 4, True), (70001, 6, False)])
-def test_encoder_fused_backward_matches_split(rows, k, gather):
+def test_encoder_fused_backward_matches_split(rows, k, gather, scratch):
     """Round 6: an encoder whose input needs no gradient trains on agn_encoder_bwd_fused (the forward
     saves nothing; h0..h3 recomputed, dW1..dW3 on chip, dW0 from G0 on agn_wgrad). Its recompute is
     bitwise the forward, so its G's equal the split path's (pinned above by the mask-matched float64
@@ -314,6 +315,7 @@ def test_encoder_fused_backward_matches_split(rows, k, gather):
 
     def run(fused):
         os.environ["AEROGNN_FUSED_ENC_BWD"] = "1" if fused else "0"
+        os.environ["AEROGNN_EB_SCRATCH"] = scratch  # a2 / a3 recomputed or parked in the scratch
         try:
             m.zero_grad(set_to_none=True)
             core.PROF = []
@@ -324,6 +326,7 @@ def test_encoder_fused_backward_matches_split(rows, k, gather):
         finally:
             core.PROF = None
             os.environ.pop("AEROGNN_FUSED_ENC_BWD", None)
+            os.environ.pop("AEROGNN_EB_SCRATCH", None)
         return y.detach().clone(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}, tags
 
     y1, g1, t1 = run(True)
