@@ -356,25 +356,27 @@ def edge_forward(*, rows, wpk, bias, ln, e, proj, src, dst, out, a1=None, stats=
 # synchronisation); a later launch reads it once the copy's event has completed. At every optimizer
 # step (a global step pre-hook, registered with the first fused launch) fault_checkpoint() raises on a
 # completed copy and enqueues one that covers the launches since the last, so the final <= 15 launches
-# of a run are read too; an atexit hook waits for the last copy. A fault is fatal to
-# the job: under torchrun the raising rank's exit ends the other ranks (they would otherwise wait in
-# the next all-reduce).
+# of a run are read too; an atexit hook waits for the last copy. A copy read
+# inside a backward only records the word: the raise happens at the step boundary (optimizer step,
+# GradAllReduce.__call__, exit). A fault is fatal to the job: under torchrun the raising rank's exit
+# ends the other ranks (they would otherwise wait in the next all-reduce).
 FAULT_POLL_EVERY = 16
-_fault = {"buf": None, "event": None, "n": 0, "dirty": False, "hooked": False}
+_fault = {"buf": None, "event": None, "n": 0, "dirty": False, "hooked": False, "word": 0}
 
 
-def _fault_read(block):
+def _fault_read(block, defer=False):
+    """Read a completed copy of the fault word. defer=True (inside a backward) only records a
+    nonzero word; the next step boundary raises it, so no rank stops in the middle of its backward
+    with all-reduce buckets in flight."""
     st = _fault
     ev = st["event"]
-    if ev is None:
-        return
-    if block:
-        ev.synchronize()
-    elif not ev.query():
-        return
-    f = int(st["buf"][0])
-    st["event"] = None
-    if f:
+    if ev is not None and (block or ev.query()):
+        if block:
+            ev.synchronize()
+        st["word"] |= int(st["buf"][0])
+        st["event"] = None
+    f = st["word"]
+    if f and not defer:
         raise L.AeroGNNError(f"fused edge backward: device fault word {f:#x} (LDS ring wait timed out; "
                              "dW of a recent step invalid)")
 
@@ -425,7 +427,7 @@ def _poll_faults():
         register_optimizer_step_pre_hook(_step_pre_hook)
         atexit.register(_exit_check)
         st["hooked"] = True
-    _fault_read(False)
+    _fault_read(False, defer=True)
     st["dirty"] = True
     st["n"] += 1
     if st["event"] is None and st["n"] >= FAULT_POLL_EVERY:

@@ -164,6 +164,10 @@ class GradAllReduce:
         self._works[bi] = all_reduce_(flat, async_op=True)
 
     def __call__(self):
+        # step boundary: a fused-backward fault word read during this backward raises here, on the
+        # faulting rank, before it waits for its buckets (aerognn/core.py fault_checkpoint)
+        from . import core
+        core.fault_checkpoint()
         if not active():
             return
         ev = None

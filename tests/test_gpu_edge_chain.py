@@ -321,7 +321,7 @@ def test_fault_checkpoint_reads_the_last_launch():
     assert L.fault_status(reset=True) == 0
     old = core.CHECK_FAULTS
     core.CHECK_FAULTS = False
-    core._fault.update(event=None, n=0, dirty=False)
+    core._fault.update(event=None, n=0, dirty=False, word=0)
     try:
         ch = Chain(51)
         src, dst = _level(3000, 70001, 52)
@@ -340,5 +340,26 @@ def test_fault_checkpoint_reads_the_last_launch():
             core.fault_checkpoint(block=True)
     finally:
         L.fault_status(reset=True)
-        core._fault.update(event=None, n=0, dirty=False)
+        core._fault.update(event=None, n=0, dirty=False, word=0)
         core.CHECK_FAULTS = old
+
+
+def test_fault_read_inside_backward_is_deferred():
+    """a nonzero fault word read by the poll inside a backward (_poll_faults) is only
+    recorded; the next step boundary (fault_checkpoint: optimizer step, GradAllReduce, exit) raises
+    it, so a rank never stops mid-backward with all-reduce buckets in flight."""
+    from aerognn import core
+    from aerognn import _lib as L
+    assert L.fault_status(reset=True) == 0
+    core._fault.update(event=None, n=0, dirty=False, word=0)
+    try:
+        assert L.lib().agn_debug_set_fault(1) == 0
+        core._fault_enqueue()
+        torch.cuda.synchronize()
+        core._poll_faults()  # reads the completed copy: records, does not raise
+        assert core._fault["word"] == 1
+        with pytest.raises(L.AeroGNNError):
+            core.fault_checkpoint()
+    finally:
+        L.fault_status(reset=True)
+        core._fault.update(event=None, n=0, dirty=False, word=0)
