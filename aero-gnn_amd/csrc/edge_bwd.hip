@@ -332,10 +332,10 @@ AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const B
 
 // SAVED: the tile starts from the forward's a1 (AGN_TILED) and LayerNorm statistics
 // (agn_edge_forward32's training saves) instead of recomputing h0 from e, P_s[src], P_d[dst] and
-// W_e; every value downstream is bitwise the same. SCR: a2 and a3 of the recompute go to the wave's
-// 16-KB slice of a.scratch (L2-resident: the same addresses are rewritten every tile) and are read
-// back for their hand-offs, instead of being recomputed from a1 a second time (64 MFMAs plus their
-// bias / ReLU work per tile).
+// W_e; every value downstream is bitwise the same. a3 stays in registers from the forward recompute
+// to its hand-off; a2 is recomputed from a1 for its own (32 MFMAs plus its bias / ReLU work per
+// tile), or with SCR parked in the wave's 8-KB slice of a.scratch and read back (opt-in: the same
+// time, and the slices do not stay in L2).
 // ENC: the same chain as an encoder MLP (models/mlp.py:40-51 on the node / edge features,
 // models/bsms_mgn.py:138-139): h0 = x W0^T + b0 on k <= 16 input features (a.e, rows gathered by
 // a.src when set), S = g (no receiver term), and no input gradient: the tile ends with G0's store
@@ -368,9 +368,8 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     const int32_t* p = (lane0 < 32 && !SAVED) ? srcp : dstp;  // (SAVED reads no src)
     return p[rr];
   };
-  // this wave's scratch slice: a2 at +0, a3 at +8 KB, unit i of lane l at 16 (64 i + l) (1 KB per
-  // wave instruction)
-  uint4* const scr = SCR ? reinterpret_cast<uint4*>(a.scratch) + (size_t)(blockIdx.x * CW + cw) * 1024 : nullptr;
+  // this wave's scratch slice (a2): unit i of lane l at 16 (64 i + l) (1 KB per wave instruction)
+  uint4* const scr = SCR ? reinterpret_cast<uint4*>(a.scratch) + (size_t)(blockIdx.x * CW + cw) * 512 : nullptr;
   if (rw.first < rw.end) ids[lane0] = tile_id(rw.first);
   for (int rd = rw.first; rd < rw.end; rd += rw.step, ++rcount) {
     const int cmax = min(CW, ntiles - rd * CW);
@@ -478,7 +477,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     acc_bias(acc, pv + 0 * H, h);
     gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
     cbarrier();
-    {  // a2 is not kept (recomputed from a1 in step 2, or parked in the scratch)
+    {  // a2 is not kept (recomputed from a1 for its hand-off, or parked in the scratch)
       BOp<bf16, NR> a2;
       a2.template set_relu<NT>(acc);
       pin(a2);
@@ -492,19 +491,14 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       gemm_rows(acc, a2, lds + 1 * IMG_B, fresh_lane(lane));
     }
     cbarrier();
-    {  // a3 is not kept either (recomputed in step 3, or parked in the scratch)
-      BOp<bf16, NR> a3;
-      a3.template set_relu<NT>(acc);
-      pin(a3);
-      if constexpr (SCR) {
-        const int l = fresh_lane(lane);
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) scr[512 + 64 * i + l] = __builtin_bit_cast(uint4, a3.u[i]);
-      }
-      sched_fence();
-      acc_bias(acc, pv + 2 * H, h);
-      gemm_rows(acc, a3, lds + 2 * IMG_B, fresh_lane(lane));
-    }
+    // a3 stays in registers from here to its hand-off (the chain recomputes only a2: one GEMM
+    // instead of two, round 6)
+    BOp<bf16, NR> a3;
+    a3.template set_relu<NT>(acc);
+    pin(a3);
+    sched_fence();
+    acc_bias(acc, pv + 2 * H, h);
+    gemm_rows(acc, a3, lds + 2 * IMG_B, fresh_lane(lane));
     EB_STAMP(2);
     // LayerNorm statistics (mlp_fwd_res_kernel's epilogue)
     float mean, rstd;
@@ -559,7 +553,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     }
     // ---- LayerNorm backward (mlp_bwd_res_kernel, its expressions; partials in 16-register
     // chunks: the butterfly's XOR order 16, 8, 4, 2, 1 gives each feature the same sums)
-    BOp<bf16, NR> a3s;  // SCR: a3 read back
     {
       const float* gmv = pv + 3 * H;
       // this wave's LayerNorm parameter partials: lane c adds sum g * xhat (c < 16) or sum g
@@ -605,11 +598,6 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
       c2 = sum32(c2);
       c1 /= (float)H;
       c2 /= (float)H;
-      if constexpr (SCR) {  // a3 back from the scratch, under the second pass
-        const int l = fresh_lane(lane);
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) a3s.u[i] = __builtin_bit_cast(bf16x8, scr[512 + 64 * i + l]);
-      }
       // pass 2 unpacks h3 and recomputes xhat again: opaque copies keep the compiler from holding
       // pass 1's 64 unpacked / normalised values live in between
       opaque(mean);
@@ -645,44 +633,28 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     op.set(A);  // G3
     pin(op);
     BOp<bf16, NR> a2;
-    if constexpr (SCR) {
-      pin(a3s);
-      EB_STAMP(4);
-      produce_pair(lds, nbase + 0 * gsz, op, a3s, fresh_lane(lane), EB_IST(0));
-      {  // a2 back from the scratch, under the chain step
-        const int l = fresh_lane(lane);
-#pragma unroll
-        for (int i = 0; i < NR / 8; ++i) a2.u[i] = __builtin_bit_cast(bf16x8, scr[64 * i + l]);
-      }
-      EB_STAMP(5);
-      gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
-      cbarrier();
-      relu_select_pk(op, acc, a3s);  // G2
-      EB_STAMP(6);
-    } else {
-      // a2 = relu(a1 W1^T + b1), a3 = relu(a2 W2^T + b2) again (the forward's operations)
-      BOp<bf16, NR> a3;
+    if constexpr (!SCR) {  // a2 = relu(a1 W1^T + b1) again (the forward's operations)
       sched_fence();
       acc_bias(acc, pv + 0 * H, h);
       gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
       cbarrier();
       a2.template set_relu<NT>(acc);
       pin(a2);
-      sched_fence();
-      acc_bias(acc, pv + 1 * H, h);
-      gemm_rows(acc, a2, lds + 1 * IMG_B, fresh_lane(lane));
-      cbarrier();
-      a3.template set_relu<NT>(acc);
-      pin(a3);
-      sched_fence();
-      EB_STAMP(4);
-      produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
-      EB_STAMP(5);
-      gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
-      cbarrier();
-      relu_select_pk(op, acc, a3);  // G2
-      EB_STAMP(6);
     }
+    pin(a3);
+    sched_fence();
+    EB_STAMP(4);
+    produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
+    if constexpr (SCR) {  // a2 back from the scratch, under the chain step
+      const int l = fresh_lane(lane);
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) a2.u[i] = __builtin_bit_cast(bf16x8, scr[64 * i + l]);
+    }
+    EB_STAMP(5);
+    gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
+    cbarrier();
+    relu_select_pk(op, acc, a3);  // G2
+    EB_STAMP(6);
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
     EB_STAMP(7);
@@ -945,7 +917,7 @@ int agn_edge_bwd_blocks(int rows) {
   return n < 8 ? 8 : n;
 }
 
-size_t agn_edge_bwd_scratch_bytes(int nblk) { return nblk > 0 ? (size_t)nblk * CW * 2 * 32 * H * 2 : 0; }
+size_t agn_edge_bwd_scratch_bytes(int nblk) { return nblk > 0 ? (size_t)nblk * CW * 32 * H * 2 : 0; }
 
 int agn_fault_status_async(int* host_pinned, void* stream) {
   if (!host_pinned) return AGN_E_ARG;

@@ -11,7 +11,7 @@ except the kernels' own roundings:
   rounding). Every output (de, G0, dW1..dW3, db1..db3, the LayerNorm partials) is gated at 3x its
   measured rel-L2.
 * the backward's variants (its recompute started from the forward's a1 / statistics or from e and
-  the projection rows; a2 / a3 parked in the L2 scratch or recomputed) are bitwise one another.
+  the projection rows; a2 parked in the scratch or recomputed) are bitwise one another.
 """
 import os
 
@@ -32,7 +32,7 @@ H = 128
 BWD_MEASURED = {"de": 2.41e-3, "g0": 3.36e-3, "dW1": 2.75e-3, "dW2": 2.32e-3, "dW3": 1.58e-3, "db1": 2.71e-3,
                 "db2": 2.34e-3, "db3": 1.59e-3, "dgamma": 1.6e-7, "dbeta": 1.5e-7}
 
-# (saved, scratch): the backward's recompute from the forward's a1 / statistics, a2 / a3 through the scratch
+# (saved, scratch): the backward's recompute from the forward's a1 / statistics, a2 through the scratch
 VARIANTS = {"saved_scratch": (True, True), "saved": (True, False), "recompute_scratch": (False, True),
             "recompute": (False, False)}
 
@@ -190,8 +190,8 @@ def test_edge_backward_mask_matched_fp64(variant, N, E, with_g):
 @pytest.mark.parametrize("N,E,with_g", [(5000, 70001, True), (300, 17, True), (20000, 100000, False),
                                         (100000, 598400, True)])
 def test_fused_backward_variants_bitwise(N, E, with_g):
-    """Round 6: the recompute started from the forward's a1 / statistics and a2 / a3 read back from
-    the L2 scratch give the round-5 kernel's outputs bit for bit (de, G0, dW, db, LayerNorm partials):
+    """Round 6: the recompute started from the forward's a1 / statistics and a2 read back from the
+    scratch give the recompute-everything kernel's outputs bit for bit (de, G0, dW, db, LayerNorm partials):
     the same operands reach the same MFMA and VALU sequences."""
     ch = Chain(31)
     src, dst = _level(N, E, 32)

@@ -315,7 +315,7 @@ def test_encoder_fused_backward_matches_split(rows, k, gather, scratch):
 
     def run(fused):
         os.environ["AEROGNN_FUSED_ENC_BWD"] = "1" if fused else "0"
-        os.environ["AEROGNN_EB_SCRATCH"] = scratch  # a2 / a3 recomputed or parked in the scratch
+        os.environ["AEROGNN_EB_SCRATCH"] = scratch  # a2 recomputed or parked in the scratch
         try:
             m.zero_grad(set_to_none=True)
             core.PROF = []

@@ -1,6 +1,6 @@
 """Same-box timing of the fused edge backward's variants (round 6) on one C3 level-0 sized layer
 (1M nodes / ~6M edges, ellipsoid mesh in CSC order): the recompute started from the forward's a1 /
-LayerNorm statistics or from e and the projection rows, and a2 / a3 parked in the L2 scratch or
+LayerNorm statistics or from e and the projection rows, and a2 parked in the scratch or
 recomputed; plus the edge forward with and without its training saves. HIP events around each
 launch, medians over REPS launches, the variants interleaved so box drift hits them alike.
 

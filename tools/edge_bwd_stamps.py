@@ -3,8 +3,8 @@ sized layer (1M nodes / ~6M edges), the -DAGN_EB_STAMPS library (AEROGNN_LIB), s
 phase of the chain waves of blocks 0 and 128 (8 tiles each) and the dW waves' wait share.
 
 Usage (GPU): AEROGNN_LIB=aero-gnn_amd/aerognn/libaerognn_stamps.so python tools/edge_bwd_stamps.py
-SAVED=1 (default): the recompute starts from the forward's a1 / statistics; SCR=1 (default): a2 / a3
-through the L2 scratch (the "recompute a2,a3" phase then covers the a3 read-back wait only).
+SAVED=1 (default): the recompute starts from the forward's a1 / statistics; SCR=1: a2 through the
+scratch (default 0: a2 recomputed from a1; a3 stays in registers from the forward recompute).
 """
 import os
 import sys
@@ -18,7 +18,7 @@ os.environ.setdefault("AEROGNN_MEMLOG", "0")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PHASES = ["ids+loads", "forward", "LN stats+bwd", "recompute a2,a3", "produce L3", "chain L3", "produce L2",
+PHASES = ["ids+loads", "forward", "LN stats+bwd", "recompute a2", "produce L3", "chain L3", "produce L2",
           "chain L2", "produce L1", "chain L1", "step 0 (de, G0)"]
 
 
@@ -50,14 +50,14 @@ def main():
     g0 = torch.empty(E, H, dtype=dt, device=dev)
 
     saved = os.environ.get("SAVED", "1") == "1"
-    scr = os.environ.get("SCR", "1") == "1"
+    scr = os.environ.get("SCR", "0") == "1"
     a1 = lnst = None
     if saved:
         a1 = core.tiled_empty(E, H, dt, e.device)
         lnst = torch.empty(E, 2, dtype=torch.float32, device=dev)
         core.edge_forward(rows=E, wpk=es.wpk(), bias=es.biases(), ln=es.lnp(), e=e, proj=P, src=lv.src, dst=lv.dst,
                           out=torch.empty_like(e), a1=a1, stats=lnst)
-    print(f"saved a1 / statistics: {saved}; a2 / a3 scratch: {scr}")
+    print(f"saved a1 / statistics: {saved}; a2 scratch: {scr}")
 
     def run():
         return core.edge_bwd_fused(rows=E, wpk=es.wpk(), wtpk0=es.wtpk()[0], bias=es.biases(), ln_g=es.lnp()[0], e=e, proj=P,
