@@ -440,8 +440,9 @@ def edge_bwd_fused(*, rows, wpk, wtpk0, bias, ln_g, e, proj, src, dst, g, g2, de
     partials [nblk, 256] fp32, nblk) after the fixed-order slab reduction (agn_wgrad_reduce).
     a1 / stats: the forward's saves (agn_edge_forward32);
     then e, proj and src are not read. scratch None: AEROGNN_EB_SCRATCH (default off) decides whether
-    a2 goes through a scratch buffer instead of a second recompute (a3 stays in registers; bitwise the
-    same outputs; not faster, and its slices leave L2: DESIGN.md §9 round 6)."""
+    a2 goes through a scratch buffer instead of a second recompute on the recompute path (with a1 /
+    stats, a2 and a3 stay in registers; bitwise the same outputs; not faster, and its slices leave L2:
+    DESIGN.md §9 round 6)."""
     import os
     lib = L.lib()
     dev = g2.device

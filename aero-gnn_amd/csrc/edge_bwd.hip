@@ -333,9 +333,10 @@ AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const B
 // SAVED: the tile starts from the forward's a1 (AGN_TILED) and LayerNorm statistics
 // (agn_edge_forward32's training saves) instead of recomputing h0 from e, P_s[src], P_d[dst] and
 // W_e; every value downstream is bitwise the same. a3 stays in registers from the forward recompute
-// to its hand-off; a2 is recomputed from a1 for its own (32 MFMAs plus its bias / ReLU work per
-// tile), or with SCR parked in the wave's 8-KB slice of a.scratch and read back (opt-in: the same
-// time, and the slices do not stay in L2).
+// to its hand-off. SAVED keeps a2 as well and drops a1 after Lin1, re-reading it from the forward's
+// save for the L1 hand-off; otherwise a2 is recomputed from a1 for its hand-off (32 MFMAs plus its
+// bias / ReLU work per tile), or with SCR parked in the wave's 8-KB slice of a.scratch and read
+// back (opt-in: the same time, and the slices do not stay in L2).
 // ENC: the same chain as an encoder MLP (models/mlp.py:40-51 on the node / edge features,
 // models/bsms_mgn.py:138-139): h0 = x W0^T + b0 on k <= 16 input features (a.e, rows gathered by
 // a.src when set), S = g (no receiver term), and no input gradient: the tile ends with G0's store
@@ -477,11 +478,15 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     acc_bias(acc, pv + 0 * H, h);
     gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
     cbarrier();
-    {  // a2 is not kept (recomputed from a1 for its hand-off, or parked in the scratch)
-      BOp<bf16, NR> a2;
+    // SAVED: a2 stays in registers to its hand-off and a1 is dropped here (re-read from the
+    // forward's save for the L1 hand-off); otherwise a2 is recomputed from a1 (or parked in the
+    // scratch) and a1 stays
+    constexpr bool KEEP2 = SAVED;
+    BOp<bf16, NR> a2;
+    {
       a2.template set_relu<NT>(acc);
       pin(a2);
-      if constexpr (SCR) {
+      if constexpr (SCR && !KEEP2) {
         const int l = fresh_lane(lane);
 #pragma unroll
         for (int i = 0; i < NR / 8; ++i) scr[64 * i + l] = __builtin_bit_cast(uint4, a2.u[i]);
@@ -632,8 +637,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     cbarrier();
     op.set(A);  // G3
     pin(op);
-    BOp<bf16, NR> a2;
-    if constexpr (!SCR) {  // a2 = relu(a1 W1^T + b1) again (the forward's operations)
+    if constexpr (!SCR && !KEEP2) {  // a2 = relu(a1 W1^T + b1) again (the forward's operations)
       sched_fence();
       acc_bias(acc, pv + 0 * H, h);
       gemm_rows(acc, a1, lds + 0 * IMG_B, fresh_lane(lane));
@@ -645,7 +649,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     sched_fence();
     EB_STAMP(4);
     produce_pair(lds, nbase + 0 * gsz, op, a3, fresh_lane(lane), EB_IST(0));
-    if constexpr (SCR) {  // a2 back from the scratch, under the chain step
+    if constexpr (SCR && !KEEP2) {  // a2 back from the scratch, under the chain step
       const int l = fresh_lane(lane);
 #pragma unroll
       for (int i = 0; i < NR / 8; ++i) a2.u[i] = __builtin_bit_cast(bf16x8, scr[64 * i + l]);
@@ -654,6 +658,13 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a3);  // G2
+    if constexpr (KEEP2) {  // a1 again, into a3's registers, two chain steps ahead of its use
+      int rr3 = rr;
+      opaque(rr3);  // (a new load, not the first one's value kept live)
+      const uint4* ap = reinterpret_cast<const uint4*>(a.a1);
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) a1.u[i] = __builtin_bit_cast(bf16x8, ap[tiled_unit<bf16, NR>(rr3, i, h)]);
+    }
     EB_STAMP(6);
     pin(op);
     produce_pair(lds, nbase + 2 * gsz, op, a2, fresh_lane(lane), EB_IST(2));
@@ -956,8 +967,7 @@ int agn_edge_bwd_fused(const agn_edge_bwd_args* a, void* stream) {
   if (!a->wtpk0) return AGN_E_ARG;
   const bool saved = a->a1 != nullptr, scr = a->scratch != nullptr;
   const dim3 grid(a->nblk), blk(NTHR);
-  if (saved && scr) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, true>), grid, blk, 0, (hipStream_t)stream, *a);
-  else if (saved) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, false>), grid, blk, 0, (hipStream_t)stream, *a);
+  if (saved) hipLaunchKernelGGL((edge_bwd_fused_kernel<true, false>), grid, blk, 0, (hipStream_t)stream, *a);  // (keeps a2: no scratch)
   else if (scr) hipLaunchKernelGGL((edge_bwd_fused_kernel<false, true>), grid, blk, 0, (hipStream_t)stream, *a);
   else hipLaunchKernelGGL((edge_bwd_fused_kernel<false, false>), grid, blk, 0, (hipStream_t)stream, *a);
   return launch_status();

@@ -390,10 +390,12 @@ typedef struct {
    * a1 (bitwise the values it would recompute) and reads no e, proj or src; NULL = recompute h0. */
   const void* a1;
   const float* stats;
-  /* optional: [nblk][4][32][128] bf16 (32 KB per block, agn_edge_bwd_scratch_bytes), the chain
-   * waves' a2 parked between the recompute and its hand-off instead of recomputed a second time
-   * from a1 (a3 stays in registers either way). Outputs are bitwise the same. Not the default: the
-   * slices do not stay in L2 and the launch is no faster. */
+  /* optional, read only without a1 / stats (with them a2 and a3 stay in registers and a1 is
+   * re-read for its hand-off): [nblk][4][32][128] bf16 (32 KB per block,
+   * agn_edge_bwd_scratch_bytes), the chain waves' a2 parked between the recompute and its hand-off
+   * instead of recomputed a second time from a1 (a3 stays in registers either way). Outputs are
+   * bitwise the same. Not the default: the slices do not stay in L2 and the launch is no faster
+   * (DESIGN.md §9 round 6). */
   void* scratch;
   /* packed A = W_e^T (agn_pack trans = 1, bf16): de = G0 W_e + S reads it from L2 (round 6: W_e's
    * LDS image went to the hand-off ring) */
