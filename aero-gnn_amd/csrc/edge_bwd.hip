@@ -8,26 +8,28 @@
 //   G3 = LN'(S);  dW3 += G3^T a3, db3 += sum G3;  G2 = (G3 W3) . [a3 > 0];  ... ;
 //   G0 = (G1 W1) . [a1 > 0];  de = G0 W_e + S.
 //   G0 is written (its sender / receiver segment sums are dP_s / dP_d, dW_e = G0^T e goes to
-//   agn_wgrad); G1..G3, a1..a3 and h3 never reach HBM, and the training forward saves nothing.
+//   agn_wgrad); G1..G3, a2, a3 and h3 never reach HBM.
 //
 // Work split (one 512-thread workgroup per CU, two waves per SIMD):
-//  * waves 0-3 ("chain waves", one per SIMD) each own a 32-edge tile per round: they recompute
-//    h0..h3 from e and the gathered projection rows (bitwise the forward kernel's values: same
-//    operands, same MFMA order), run the LayerNorm backward and the chain rule, and hand each
-//    layer's (G_L, a_L) to the dW waves in 16-row items through an LDS ring;
+//  * waves 0-3 ("chain waves", one per SIMD) each own a 32-edge tile per round. They start from
+//    the forward's saved a1 and LayerNorm statistics (agn_edge_forward32's training saves; without
+//    them h0 is recomputed from e, P_s[src], P_d[dst] and W_e), recompute h1..h3 bitwise the
+//    forward kernel's values (same operands, same MFMA order), keep a2 and a3 in registers, run the
+//    LayerNorm backward and the chain rule, and hand each layer's (G_L, a_L) to the dW waves in
+//    16-row items through an LDS ring;
 //  * waves 4-7 ("dW waves", one per SIMD) own a 64x64 quarter of dW1..dW3 each (192 accumulator
-//    registers for the whole launch) and consume every item in a fixed order (round, layer,
-//    half, chain wave): the fp32 sums are deterministic;
-//  * all four Linears live in LDS as ONE image each, read both ways: rows (ds_read_b128, the
-//    forward's A = W fragments) and columns (ds_read_b64_tr_b16, the backward's A = W^T
-//    fragments). The image is layout (a) of cdna_hip_programming.md T10 over the packed forward
-//    operand (agn_pack, trans = 0), whose k order is the acc-register order of common.hpp; the
-//    transposed reads pick their 8-byte pieces so that each lane gets the same 8 values, in the
-//    same order, as the split path's packed W^T fragments (agn_pack, trans = 1).
-// The ring holds 3 slots of 8 KB (G_L and a_L for 16 rows, layout (a) images read with
-// ds_read_b64_tr_b16 by the dW MFMAs, k = rows). A chain wave writes item n into slot n % 3 once
-// item n - 3 has been consumed by all four dW waves; LDS counters (filled / consumed) order the
-// hand-offs, no workgroup barrier runs inside the main loops.
+//    registers for the whole launch) and consume every item in a fixed order (round, wave group,
+//    layer, wave, half): the fp32 sums are deterministic;
+//  * Lin1..Lin3 live in LDS as ONE image each, read both ways: rows (ds_read_b128, the forward's
+//    A = W fragments) and columns (ds_read_b64_tr_b16, the backward's A = W^T fragments). The image
+//    is layout (a) of cdna_hip_programming.md T10 over the packed forward operand (agn_pack,
+//    trans = 0), whose k order is the acc-register order of common.hpp; the transposed reads pick
+//    their 8-byte pieces so that each lane gets the same 8 values, in the same order, as the split
+//    path's packed W^T fragments (agn_pack, trans = 1). W_e's packed fragments are read from L2.
+// The ring holds NSLOT (7) slots of 8 KB (G_L and a_L for 16 rows, layout (a) images read with
+// ds_read_b64_tr_b16 by the dW MFMAs, k = rows). A chain wave writes item n into slot n % NSLOT
+// once item n - NSLOT has been consumed by all four dW waves; LDS counters (filled / consumed)
+// order the hand-offs, no workgroup barrier runs inside the main loops.
 // Per-workgroup partials (dW, db, LayerNorm) go to slabs that agn_wgrad_reduce / agn_colsum sum in
 // fixed order: no atomics on HBM.
 #include "common.hpp"
@@ -241,6 +243,18 @@ struct Rounds {  // XCD-grouped round walk (blocks b and b + 8 share an XCD and 
 // rows 16 half .. 16 half + 15 of the wave's tile, as two layout (a) images: unit i of lane
 // (c, hh) = positions 16i + 8hh..+7 (chunk 2i + hh) of row c & 15. A chain wave hands both halves
 // over at once (items n0, n0 + 1): every lane writes, each half into its own slot.
+// an item pair's filled flags, once this wave's writes of it have retired (LDS in order per wave)
+AGN_DEV void produce_flag(char* lds, int n0, int lane) {
+#ifdef AGN_EB_NORING
+  return;
+#endif
+  int* filled = reinterpret_cast<int*>(lds + OFF_FLAG);
+  lgkm_drain();
+  if (lane == 0) {
+    __hip_atomic_store(&filled[n0 % NSLOT], n0 / NSLOT + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&filled[(n0 + 1) % NSLOT], (n0 + 1) / NSLOT + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
 AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<bf16, NR>& X, int lane,
                           unsigned long long* ist = nullptr) {
 #ifdef AGN_EB_NORING
@@ -269,11 +283,8 @@ AGN_DEV void produce_pair(char* lds, int n0, const BOp<bf16, NR>& G, const BOp<b
     *reinterpret_cast<uint4*>(sb + o) = __builtin_bit_cast(uint4, G.u[i]);
     *reinterpret_cast<uint4*>(sb + HALF_B + o) = __builtin_bit_cast(uint4, X.u[i]);
   }
-  lgkm_drain();
-  if (lane == 0) {
-    __hip_atomic_store(&filled[k0], j0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_store(&filled[k1], j1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
+  // the flags are set by produce_flag after the chain step that follows (its LDS waits retire these
+  // writes, so that drain costs nothing; round 6: -0.8 % per launch)
 #ifdef AGN_EB_STAMPS
   if (ist && lane == 0) ist[2] = __builtin_amdgcn_s_memtime();
 #endif
@@ -658,6 +669,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     gemm_cols(acc, op, lds + 2 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a3);  // G2
+    produce_flag(lds, nbase + 0 * gsz, fresh_lane(lane));
     if constexpr (KEEP2) {  // a1 again, into a3's registers, two chain steps ahead of its use
       int rr3 = rr;
       opaque(rr3);  // (a new load, not the first one's value kept live)
@@ -672,6 +684,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     gemm_cols(acc, op, lds + 1 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a2);  // G1
+    produce_flag(lds, nbase + 2 * gsz, fresh_lane(lane));
     EB_STAMP(8);
     pin(op);
     // de = G0 W_e + (g + g2) (mlp_bwd_res_kernel's add_grad_w order) needs the incoming rows
@@ -696,6 +709,7 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     gemm_cols(acc, op, lds + 0 * IMG_B, fresh_lane(lane));
     cbarrier();
     relu_select_pk(op, acc, a1);  // G0
+    produce_flag(lds, nbase + 4 * gsz, fresh_lane(lane));
     EB_STAMP(10);
     pin(op);
     if (more) ids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
