@@ -306,10 +306,11 @@ STAMPS = None  # diagnostics: a uint64 device tensor of 2*8*8*16 entries (a -DAG
 
 def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
     """agn_edge_bwd_fused applies: bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN) large
-    enough for the persistent kernels. Then the training forward saves nothing for the edge chain
-    and one launch recomputes it in the backward (csrc/edge_bwd.hip): 418 instead of 710 GB of
-    HBM traffic per C3 train step and ≈7 % less time. AEROGNN_FUSED_EDGE_BWD=0
-    selects the split path (saved activations, agn_mlp_backward + agn_wgrad) for A/B tests."""
+    enough for the persistent kernels. Then the training forward saves only a1 and the LayerNorm
+    statistics of the edge chain (edge_saves_ok) and one launch recomputes the rest in the backward
+    (csrc/edge_bwd.hip): 422 instead of 680 GB of HBM traffic per C3 train step (DESIGN.md §9,
+    rounds 3 and 6). AEROGNN_FUSED_EDGE_BWD=0 selects the split path (saved activations,
+    agn_mlp_backward + agn_wgrad) for A/B tests."""
     import os
     return (os.environ.get("AEROGNN_FUSED_EDGE_BWD", "1") != "0" and dtype == torch.bfloat16 and hidden == 128
             and nlin == 4 and has_ln and rows >= 64 * 1024)
