@@ -326,13 +326,17 @@ AGN_DEV void relu_select_pk(BOp<bf16, NR>& out, const f32x16 (&acc)[NT], const B
 // into a.stamps[((sel * 8 + w) * 8 + tile) * 16 + point]; dW wave d stores its total wait and
 // total cycles at point 0 / 1 of slot (sel * 8 + 4 + d) * 8 * 16.
 #ifdef AGN_EB_STAMPS
+#ifndef AGN_EB_STAMP_MASK
+#define AGN_EB_STAMP_MASK 0xfff  // which of the 12 points are stamped (1: the tile starts only)
+#endif
 #define EB_STAMP(k)                                                                                     \
   do {                                                                                                  \
-    if (stp && ntile_done < 8 && (lane0 & 63) == 0) stp[ntile_done * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+    if (((AGN_EB_STAMP_MASK >> (k)) & 1) && stp && ntile_done < 8 && (lane0 & 63) == 0)                \
+      stp[ntile_done * 16 + (k)] = __builtin_amdgcn_s_memtime();                                        \
   } while (0)
 // item-level clocks of produce(): tiles 1 and 2 of block 0's chain waves, at 2048 + 576 + ..
 #define EB_IST(pi) \
-  ((stp && blockIdx.x == 0 && (ntile_done == 1 || ntile_done == 2)) \
+  ((AGN_EB_STAMP_MASK == 0xfff && stp && blockIdx.x == 0 && (ntile_done == 1 || ntile_done == 2)) \
        ? a.stamps + 2048 + 576 + ((cw * 2 + ntile_done - 1) * 6 + (pi)) * 3 : nullptr)
 #else
 #define EB_STAMP(k) \
