@@ -5,6 +5,9 @@
 // the same exact MFMA row sum P_s + P_d, the same LayerNorm and residual steps), so the 32-row
 // fused backward (edge_bwd.hip), which recomputes that kernel's chain, pairs with it unchanged.
 //
+// The residual add round(LN(h3)) + e runs on the matrix cores like the row sum (round 6: 160 VALU
+// fewer per tile, -1 % per launch).
+//
 // Why a second kernel: the chain is vector-issue-bound on the SIMD, not HBM- or MFMA-bound
 // (DESIGN.md §9 round 5). A v_mfma_f32_32x32x16_bf16 holds the SIMD's vector issue for 8 of its
 // 32 cycles; the exact MFMA row sum replaces ~190 VALU unpack/add instructions per tile. Against the
@@ -39,11 +42,8 @@ constexpr int LAYER = NT * NU * 64;     // packed units (16 B) per weight image
 #define AGN_E32_PF 2
 #endif
 constexpr int PF = AGN_E32_PF;          // weight fragments in flight
-#ifndef AGN_E32_A1
-#define AGN_E32_A1 0  // where the a1 training save is stored (A/B builds: 1 behind Lin1's MFMAs, 2 non-temporal, 3 none)
-#endif
 #ifndef AGN_E32_DIAG
-#define AGN_E32_DIAG 0  // timing diagnostics only (tools/fwd_probe.py): 1 no LayerNorm, 2 no residual, 3 no row sum
+#define AGN_E32_DIAG 0  // timing diagnostics only (outputs wrong): 1 no LayerNorm statistics, 3 no row sum
 #endif
 
 constexpr int NW = 12;  // waves per CU (three per SIMD)
@@ -186,16 +186,8 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
     for (int l = 1; l < 4; ++l) {
       cbarrier();
       b.template set_relu<NT>(acc);
-      if constexpr (SAVE && AGN_E32_A1 == 0) {
-        if (l == 1) b.store_tiled(reinterpret_cast<bf16*>(a.act[0]), row, h, valid);  // a1 (AGN_TILED)
-      }
-      if constexpr (SAVE && AGN_E32_A1 == 2) {  // (A/B: non-temporal stores)
-        if (l == 1 && valid) {
-          u32x4* base = reinterpret_cast<u32x4*>(a.act[0]);
-#pragma unroll
-          for (int i = 0; i < NR / 8; ++i)
-            __builtin_nontemporal_store(__builtin_bit_cast(u32x4, b.u[i]), base + tiled_unit<bf16, NR>(row, i, h));
-        }
+      if constexpr (SAVE) {  // a1 (AGN_TILED); behind Lin1's MFMAs or non-temporal: no faster (round 6)
+        if (l == 1) b.store_tiled(reinterpret_cast<bf16*>(a.act[0]), row, h, valid);
       }
 #pragma unroll
       for (int q = 0; q < 4 * NT; ++q) {  // acc = bias of Linear l (mlp.hip acc_bias_lds)
@@ -204,9 +196,6 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
         for (int e = 0; e < 4; ++e) acc[q / 4][4 * (q % 4) + e] = x[e];
       }
       gemm4(acc, b, sm.w + l * LAYER, lane);
-      if constexpr (SAVE && AGN_E32_A1 == 1) {  // (A/B: a1 stored behind the Lin1 MFMAs)
-        if (l == 1) b.store_tiled(reinterpret_cast<bf16*>(a.act[0]), row, h, valid);
-      }
       E32_STAMP(2 + l);
     }
     cbarrier();
@@ -226,35 +215,42 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
     }
     E32_STAMP(6);
     bf16* op = reinterpret_cast<bf16*>(a.out) + (size_t)row * H;
+    {
+      // LN(h3) rounded to bf16 (the operand's packing), then round(LN) + e on the matrix cores: the
+      // identity-fragment sum of two bf16 rows is the VALU path's fp32 add bit for bit (a -0 sum
+      // comes out +0), and it replaces 160 unpack / add VALU per tile
+      float v[NR];
+#pragma unroll
+      for (int i = 0; i < NR / 8; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int f0 = 16 * i + 8 * j + 4 * h;
+          const f32x4 g4 = *reinterpret_cast<const f32x4*>(&sm.pv[3][f0]);
+          const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sm.pv[4][f0]);
+#pragma unroll
+          for (int e = 0; e < 4; e += 2) {
+            const int r = 8 * i + 4 * j + e;
+            const f32x2 o = ln_out2(f2(acc[r / 16][r % 16], acc[(r + 1) / 16][(r + 1) % 16]), mean, rstd,
+                                    f2(g4[e], g4[e + 1]), f2(b4[e], b4[e + 1]));
+            v[r] = o[0];
+            v[r + 1] = o[1];
+          }
+        }
+      }
+      BOp<bf16, NR> lnb;
+      lnb.set(v);
+      bf16x8 f0, f1;
+      ident_frags(f0, f1, lane);
+      acc_add2_mfma<NT, NR>(acc, lnb, e0, f0, f1);
+    }
 #pragma unroll
     for (int i = 0; i < NR / 8; ++i) {
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = acc[(8 * i + e) / 16][(8 * i + e) % 16];
-#pragma unroll
-      for (int j = 0; j < (AGN_E32_DIAG == 1 ? 0 : 2); ++j) {
-        const int f0 = 16 * i + 8 * j + 4 * h;
-        const f32x4 g4 = *reinterpret_cast<const f32x4*>(&sm.pv[3][f0]);
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(&sm.pv[4][f0]);
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const f32x2 o = ln_out2(f2(v[4 * j + e], v[4 * j + e + 1]), mean, rstd, f2(g4[e], g4[e + 1]),
-                                  f2(b4[e], b4[e + 1]));
-          v[4 * j + e] = o[0];
-          v[4 * j + e + 1] = o[1];
-        }
-      }
-      float r[8];
-      e0.get8(r, i);
-#pragma unroll
-      for (int e = 0; e < (AGN_E32_DIAG == 2 ? 0 : 8); e += 2) {  // round(LN) + residual, rounded again at the store
-        const uint32_t p = pack2(v[e], v[e + 1]);
-        const f32x2 o = f2(lo_bf16(p), hi_bf16(p)) + f2(r[e], r[e + 1]);
-        v[e] = o[0];
-        v[e + 1] = o[1];
-      }
       store8_w(op, i, h, v, valid);
     }
+
     E32_STAMP(7);
 #ifdef AGN_E32_STAMPS
     ++ntile;
