@@ -753,6 +753,35 @@ AGN_DEV void ident_frags(bf16x8& f0, bf16x8& f1, int lane) {
   f0 = __builtin_bit_cast(bf16x8, i < 16 ? w : z);
   f1 = __builtin_bit_cast(bf16x8, i < 16 ? z : w);
 }
+// The same identity for operands in ROW order, as 16-B loads of a row-major bf16 row deliver them
+// (lane half h holds features 16 u + 8 h .. + 7 of k-step u: no lane-half exchange, set_w): the one
+// for output row i < 16 of k-step 2 ot sits at j = i & 7 of the lanes with (i >> 3) & 1 == l >> 5.
+// The products and sums are the acc-order identity's, so acc_add2_mfma_rows(x raw, y raw) is
+// acc_add2_mfma(set_w(x), set_w(y)) bit for bit, without the 96 moves / swaps of the exchange.
+AGN_DEV void ident_frags_rows(bf16x8& f0, bf16x8& f1, int lane) {
+  const int i = lane & 31, il = i & 15;
+  const int j = il & 7;
+  const uint32_t one = (((il >> 3) & 1) == (lane >> 5)) ? (0x3F80u << (16 * (j & 1))) : 0u;
+  const int d = j >> 1;
+  const u32x4 w = {d == 0 ? one : 0u, d == 1 ? one : 0u, d == 2 ? one : 0u, d == 3 ? one : 0u};
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  f0 = __builtin_bit_cast(bf16x8, i < 16 ? w : z);
+  f1 = __builtin_bit_cast(bf16x8, i < 16 ? z : w);
+}
+template <int NT, int NU>
+AGN_DEV void acc_add2_mfma_rows(f32x16 (&acc)[NT], const uint4 (&x)[NU], const uint4 (&y)[NU], const bf16x8& f0,
+                                const bf16x8& f1) {
+  static_assert(NU == 2 * NT, "two raw 16-B chunks per output tile");
+  auto u = [](const uint4& v) { return __builtin_bit_cast(bf16x8, v); };
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, u(x[2 * ot]), f32x16{}, 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, u(x[2 * ot + 1]), acc[ot], 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f0, u(y[2 * ot]), acc[ot], 0, 0, 0);
+#pragma unroll
+  for (int ot = 0; ot < NT; ++ot) acc[ot] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f1, u(y[2 * ot + 1]), acc[ot], 0, 0, 0);
+}
 template <int NT, int NR>
 AGN_DEV void acc_add2_mfma(f32x16 (&acc)[NT], const BOp<bf16, NR>& x, const BOp<bf16, NR>& y, const bf16x8& f0,
                            const bf16x8& f1) {

@@ -150,7 +150,6 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       const int cs = wids[c], cd = wids[32 + c];
       if (more) wids[lane] = nid;  // (this tile's reads of the slot are done: LDS is in order per wave)
       // acc = P_s[src] + P_d[dst] on the matrix cores (exact fp32 add, common.hpp acc_add2_mfma)
-      BOp<bf16, NR> xs, xd;
       uint4 rs[NR / 8], rd[NR / 8];
       const bf16* ps = P + (size_t)cs * (2 * H) + 8 * h;
       const bf16* pd = P + (size_t)cd * (2 * H) + H + 8 * h;
@@ -164,18 +163,13 @@ __global__ __launch_bounds__(64 * NW) void edge32_fwd_kernel(const agn_edge_fwd_
       // SAVE instantiation (a1 / statistics stores, 152 registers) issued the P_d rows two at a time
       // behind vmcnt(0) waits (1.01 -> 1.46 ms per C3 launch)
       __builtin_amdgcn_sched_barrier(0);
-      xs.set_w(rs);
-      xd.set_w(rd);
       bf16x8 f0, f1;
-      ident_frags(f0, f1, lane);
+      ident_frags_rows(f0, f1, lane);
       if (AGN_E32_DIAG == 3) {
 #pragma unroll
-        for (int ot = 0; ot < NT; ++ot) {
-          acc[ot] = f32x16{};
-          acc[ot][0] = (float)xs.u[2 * ot][0] + (float)xd.u[2 * ot][0];
-        }
+        for (int ot = 0; ot < NT; ++ot) acc[ot] = f32x16{};
       } else {
-        acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+        acc_add2_mfma_rows<NT, NR / 8>(acc, rs, rd, f0, f1);  // rows as loaded: no lane-half exchange
       }
     }
     E32_STAMP(1);

@@ -471,12 +471,17 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
     } else if constexpr (!SAVED) {
       {
         {  // acc = P_s[src] + P_d[dst] on the matrix cores (the forward kernel's exact add)
-          BOp<bf16, NR> xs, xd;
-          xs.load_w(P + (size_t)sid * (2 * H), h);
-          xd.load_w(P + (size_t)did * (2 * H) + H, h);
+          uint4 xs[NR / 8], xd[NR / 8];  // rows as loaded (row-order identity: no lane-half exchange)
+          const bf16* ps = P + (size_t)sid * (2 * H) + 8 * h;
+          const bf16* pd = P + (size_t)did * (2 * H) + H + 8 * h;
+#pragma unroll
+          for (int i = 0; i < NR / 8; ++i) {
+            xs[i] = *reinterpret_cast<const uint4*>(ps + 16 * i);
+            xd[i] = *reinterpret_cast<const uint4*>(pd + 16 * i);
+          }
           bf16x8 f0, f1;
-          ident_frags(f0, f1, fresh_lane(lane));
-          acc_add2_mfma<NT, NR>(acc, xs, xd, f0, f1);
+          ident_frags_rows(f0, f1, fresh_lane(lane));
+          acc_add2_mfma_rows<NT, NR / 8>(acc, xs, xd, f0, f1);
         }
         BOp<bf16, NR> eop;
         eop.load_w(reinterpret_cast<const bf16*>(a.e) + (size_t)rr * H, h);
@@ -558,12 +563,9 @@ AGN_DEV void chain_wave(const agn_edge_bwd_args& a, char* lds, int cw, int lane0
         for (int e = 0; e < 8; ++e) A[8 * i + e] = x[e];
       }
     } else {  // S = g + g2 on the matrix cores (exact fp32 add): acc is free once h3 is packed
-      BOp<bf16, NR> og, og2;
-      og.set_w(graw);
-      og2.set_w(g2raw);
       bf16x8 f0, f1;
-      ident_frags(f0, f1, fresh_lane(lane));
-      acc_add2_mfma<NT, NR>(acc, og, og2, f0, f1);
+      ident_frags_rows(f0, f1, fresh_lane(lane));
+      acc_add2_mfma_rows<NT, NR / 8>(acc, graw, g2raw, f0, f1);
 #pragma unroll
       for (int i = 0; i < NR; ++i) A[i] = acc[i / 16][i % 16];
     }
