@@ -783,10 +783,8 @@ AGN_DEV void dw_wave(const agn_edge_bwd_args& a, char* lds, int d, int lane) {
       for (int y = 0; y < 2; ++y) dw[l][x][y] = f32x16{};
     }
   int n = 0, pre0 = 0, pre1 = 0;
-  // the dW waves outrank their SIMD's chain wave: their four MFMAs per item issue between the
-  // chain's instead of queueing behind a whole 32-MFMA chain step (which holds the ring slot
-  // the other chain waves are waiting for)
-  __builtin_amdgcn_s_setprio(2);
+  // (no s_setprio: until round 6 the dW waves ran at priority 2 so that their MFMAs issued between
+  // the chain's; with the faster chain, equal priority is 2.7 % faster per launch)
 #ifdef AGN_EB_STAMPS
   unsigned long long waited = 0;
   const unsigned long long tstart = __builtin_amdgcn_s_memtime();
