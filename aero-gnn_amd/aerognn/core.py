@@ -308,7 +308,7 @@ def fused_edge_train_ok(rows, dtype, hidden, nlin, has_ln):
     """agn_edge_bwd_fused applies: bf16 H=128 sum-trick edge chains (W_e + 3 Linears + LN) large
     enough for the persistent kernels. Then the training forward saves only a1 and the LayerNorm
     statistics of the edge chain (edge_saves_ok) and one launch recomputes the rest in the backward
-    (csrc/edge_bwd.hip): 417 instead of 680 GB of HBM traffic per C3 train step (DESIGN.md §9,
+    (csrc/edge_bwd.hip): 414 instead of 680 GB of HBM traffic per C3 train step (DESIGN.md §9,
     rounds 3 and 6). AEROGNN_FUSED_EDGE_BWD=0 selects the split path (saved activations,
     agn_mlp_backward + agn_wgrad) for A/B tests."""
     import os
